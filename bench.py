@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: HC paths/s of the MI355X GPU-HC tracker (trifocal_2op1p_30x30).
+
+Workload (BASELINE.json configs[1], per GPU): 100 RANSAC samples x 312 tracks,
+Abort_RANSAC=false, synthcurves dataset 000, samples drawn with srand(0) in the
+reference's gpu-major order (rank g takes its own contiguous shard of
+100*N samples).  One "step" = reset the tracks to the start solutions + one
+tracking launch over the rank's samples, inputs already resident in HBM.
+
+Multi-GPU: one process per GPU (torch.distributed, backend nccl == RCCL);
+samples are independent so the ranks share nothing on the data path (weak
+scaling); RCCL only carries the barrier and the max-over-ranks timing.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--samples S] [--no-cpu-baseline]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# SURVEY.md §8(d) algorithmic work per unit (flop convention: complex mul 6,
+# complex add 2, real x complex 2, complex div 11)
+FLOP_PRED_STAGE = 104.3e3    # Hx 12,276 + Ht 12,960 + LU 78,670 + axpys ~360
+FLOP_CORR_STAGE = 101.3e3    # Hx 12,276 + H 10,080 + LU 78,670 + update/norms ~300
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak == FP32 MFMA peak
+HBM_PEAK_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--samples", type=int, default=100, help="RANSAC samples per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-samples", type=int, default=24, help="samples in the bounded CPU baseline run")
+    ap.add_argument("--abort-samples", type=int, default=1000,
+                    help="samples of the early-abort (config 3) time-to-first-good-pose run; 0 disables")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import (_abi, load_problem, load_ransac_data,
+                                                                   prepare_target_params)
+    from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker
+
+    problem = load_problem()
+    data = load_ransac_data(0)
+    S = args.samples
+    total = S * world
+    tgt_all, dif_all, _ = prepare_target_params(problem, data, seed=0, num_samples=total, num_gpus=world)
+    # gpu-major shard of this rank (GPU_HC_Solver.cpp:85-88,263-265): equal shards here
+    tgt = torch.from_numpy(tgt_all[rank * S:(rank + 1) * S]).to(dev)
+    dif = torch.from_numpy(dif_all[rank * S:(rank + 1) * S]).to(dev)
+
+    tr = DeviceTracker(problem, dev)
+    res = tr.allocate(S, stats=True)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        tr.reset_tracks(res)
+        tr.launch(tgt, dif, res, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    # timed region: barrier + sync on both sides; per-launch kernel time with events on the launch stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        tr.reset_tracks(res)
+        ev[i][0].record(stream)
+        tr.launch(tgt, dif, res, stream=stream)
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+
+    host = res.host()
+    steps_sum = int(host["stats"]["steps"].astype(np.int64).sum())
+    corr_sum = int(host["stats"]["corrections"].astype(np.int64).sum())
+    flops = steps_sum * 4 * FLOP_PRED_STAGE + corr_sum * FLOP_CORR_STAGE
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import count_solutions
+    counts = count_solutions(host["tracks"], host["converge"], host["infinity"])
+
+    t_max = elapsed
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_max = float(tt.item())
+        fl = torch.tensor([flops, float(np.median(launch_ms))], dtype=torch.float64, device=dev)
+        dist.all_reduce(fl, op=dist.ReduceOp.SUM)
+
+    ms_per_step = t_max / args.steps * 1e3
+    paths = 312 * S * world
+    value = paths / (ms_per_step / 1e3)
+
+    # ---- early-abort (config 3) time-to-first-good-pose, rank-local, reported only
+    abort_info = None
+    if args.abort_samples > 0 and rank == 0:
+        Sa = args.abort_samples
+        ta, da, _ = prepare_target_params(problem, data, seed=0, num_samples=Sa)
+        ta = torch.from_numpy(ta).to(dev)
+        da = torch.from_numpy(da).to(dev)
+        tr.set_ransac_data(data)
+        ra = tr.allocate(Sa, stats=True, abort=True)
+        ttfp, wall = [], []
+        for _ in range(3):
+            tr.reset_tracks(ra)
+            torch.cuda.synchronize(dev)
+            w0 = time.perf_counter()
+            tr.launch(ta, da, ra, abort=True, stream=stream)
+            torch.cuda.synchronize(dev)
+            wall.append(time.perf_counter() - w0)
+            ttfp.append(tr.first_found_seconds())
+        ha = ra.host()
+        abort_info = {"samples": Sa, "found": bool(ha["found"]),
+                      "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3),
+                      "kernel_exit_wall_ms": round(float(np.median(wall)) * 1e3, 3),
+                      "paths_tracked": int((ha["stats"]["steps"] > 0).sum())}
+
+    if rank == 0:
+        med_launch_s = float(np.median(launch_ms)) / 1e3
+        achieved_tf = flops / med_launch_s / 1e12
+        line = {
+            "metric": "HC paths/sec (312 tracks x RANSAC samples)",
+            "value": round(value, 1),
+            "unit": "paths/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic RANSAC samples from the reference's synthcurves data (Triplet_Edgels_000, srand(0))",
+            "config": {"workload": "trifocal_2op1p_30x30 config 2: 100 RANSAC samples x 312 tracks per GPU, "
+                                   "Abort_RANSAC=false",
+                       "samples_per_gpu": S, "tracks_per_sample": 312, "paths_per_step": paths,
+                       "parallelism": f"samples sharded over {world} GPU(s), no data-path collective",
+                       "GPUHC_Max_Steps": tr.settings.max_steps,
+                       "GPUHC_Max_Correction_Steps": tr.settings.max_corrections,
+                       "kernel": _abi.lib().hc_trifocal_version().decode()},
+            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "note": "FP32-compute (VALU) bound tracker kernel; MI355X FP32 vector peak == FP32 MFMA "
+                                 "peak (157.3 TF). achieved = algorithmic FLOPs of the executed stages "
+                                 "(SURVEY 8d: 104.3 kFLOP/predictor stage, 101.3 kFLOP/corrector stage) / median "
+                                 "launch time (HIP events on the launch stream)",
+                         "kernel_ms": round(float(np.median(launch_ms)), 4),
+                         "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
+                         "rk4_steps": steps_sum, "corrections": corr_sum},
+            "solutions": {"converged": counts[0], "real": counts[1], "infinity": counts[2]},
+        }
+        if abort_info is not None:
+            line["early_abort"] = abort_info
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(problem, data, args.cpu_samples, value)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(problem, data, n_samples, gpu_value):
+    """The oracle's CPU-HC restatement (CPUHC_Generic_Solver_Eval_by_Indx semantics,
+    OpenMP dynamic over paths) timed on this host's cores on a bounded sample."""
+    from oracle import oracle as O
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import prepare_target_params
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    tgt, dif, _ = prepare_target_params(problem, data, seed=0, num_samples=n_samples)
+    s = O.settings(threads=threads)
+    _, _, _, _, secs = O.cpuhc_track(problem.start_sols, problem.start_params, tgt, dif,
+                                     problem.dHdx_index, problem.dHdt_index, s)
+    v = 312 * n_samples / secs
+    return {"value": round(v, 1), "unit": "paths/s", "cores": threads, "kind": "port",
+            "sample": f"CPU-HC restatement (oracle/hc_oracle.c orc_cpuhc_track, no path pruning, LAPACK-style "
+                      f"cgesv) on samples 0..{n_samples - 1} ({312 * n_samples} paths), {secs:.1f} s wall",
+            "gpu_over_cpu": round(gpu_value / v, 1)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * hc_trifocal.h -- the drop-in C-ABI boundary of the MI355X-native GPU-HC path
+ * tracker for the trifocal_2op1p_30x30 minimal problem.
+ *
+ * Replaces the four host launchers of the reference
+ *   magmaHC/gpu-kernels/magmaHC-kernels.hpp:24-105
+ *     kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths[_Volta]            (:24-61)
+ *     kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_TrunRANSAC[_Volta] (:63-105)
+ * implemented at
+ *   magmaHC/gpu-kernels/kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths.cu:292-386
+ *   magmaHC/gpu-kernels/kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_TrunRANSAC.cu:329-455
+ * and called from GPU_HC_Solver::Solve_by_GPU_HC (magmaHC/GPU_HC_Solver.cpp:390-436).
+ *
+ * Rules of the boundary:
+ *   - plain pointers and sizes, no MAGMA / torch types; hcComplex is
+ *     layout-compatible with magmaFloatComplex / cuFloatComplex / float2;
+ *   - every buffer is allocated and freed by the caller; the entry points never
+ *     allocate, copy to/from the host or synchronise (hipGraph-capturable);
+ *   - work is enqueued on the caller's stream on the CURRENT device, which is
+ *     never changed; re-entrant across devices/streams;
+ *   - errors are returned as hcStatus, never exit();
+ *   - result index space is the reference's: batch id b = sample*312 + track.
+ */
+#ifndef HC_TRIFOCAL_H
+#define HC_TRIFOCAL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HC_NUM_VARS      30   /* Num_Of_Vars   (gpuhc_settings.yaml:17)  */
+#define HC_NUM_PARAMS    33   /* Num_Of_Params (gpuhc_settings.yaml:18)  */
+#define HC_NUM_TRACKS    312  /* Num_Of_Tracks (gpuhc_settings.yaml:19)  */
+#define HC_UNIFIED_INDEX_SIZE 38880 /* 36000 dH/dx + 2880 dH/dt ints (Data_Reader.cpp:167-189) */
+
+typedef struct { float re, im; } hcComplex;         /* == magmaFloatComplex */
+typedef void *hcStream;                             /* == hipStream_t       */
+
+typedef enum {
+    HC_SUCCESS = 0,
+    HC_ERROR_INVALID_VALUE = 1,   /* bad size / null required pointer            */
+    HC_ERROR_WORKSPACE = 2,       /* workspace missing or too small               */
+    HC_ERROR_LAUNCH = 3,          /* hipLaunchKernel / hipMemsetAsync failed      */
+    HC_ERROR_DEVICE = 4,          /* no device / unsupported device (not gfx950)  */
+    HC_ERROR_TABLE = 5            /* index table exceeds the kernel's compaction capacity */
+} hcStatus;
+
+/* Optional per-path counters (one per batch id).  steps = RK4 predictor
+   executions, corrections = corrector iterations; inliers = abort-mode
+   reprojection inlier counts of the hypothesis scoring (0 otherwise). */
+typedef struct {
+    int32_t steps;
+    int32_t corrections;
+    int32_t inliers21;
+    int32_t inliers31;
+} hcPathStats;
+
+/* Tracker tuning knobs (GPUHC_* keys of gpuhc_settings.yaml:12-14). */
+typedef struct {
+    int max_steps;          /* GPUHC_Max_Steps                        (80) */
+    int max_corrections;    /* GPUHC_Max_Correction_Steps             (3)  */
+    int delta_t_inc_steps;  /* GPUHC_Num_Of_Steps_to_Increase_Delta_t (4)  */
+} hcTrackSettings;
+
+/* Arguments of one tracking launch over sub_ransac_iters samples (one GPU's share).
+ * Layouts (reference GPU_HC_Solver.cpp:137-184,335-362):
+ *   start_sols    312 x 31 complex, ld 31 (x[30] = 1)
+ *   tracks        (312*N) x 31 complex, ld 31, in/out; initialised by the caller
+ *                 to the start solutions (Feed_Start_Sols_for_Intermediate_Homotopy);
+ *                 entries 0..29 of each track are written, entry 30 is not
+ *   start_params  34 complex (p[33] = 1)
+ *   target/diff   34 complex per sample, contiguous
+ *   unified_index 38880 int32: dHdx_indx.txt || dHdt_indx.txt (the reference's
+ *                 d_unified_dHdx_dHdt_Index)
+ *   converge/infinity  one byte per batch id (bool layout)
+ * Alternatively start_sols_array / track_array may point to device arrays of
+ * 312 / 312*N per-track pointers (the reference's magma_cset_pointer arrays);
+ * when non-NULL they take precedence over the base pointers. */
+typedef struct {
+    int sub_ransac_iters;                 /* N samples on this device            */
+    hcTrackSettings settings;
+    const hcComplex *start_sols;          /* d_startSols base                    */
+    const hcComplex *const *start_sols_array; /* optional d_startSols_array      */
+    hcComplex *tracks;                    /* d_Track base                        */
+    hcComplex *const *track_array;        /* optional d_Track_array              */
+    const hcComplex *start_params;        /* d_startParams                       */
+    const hcComplex *target_params;       /* d_targetParams                      */
+    const hcComplex *diff_params;         /* d_diffParams                        */
+    const int32_t *unified_index;         /* d_unified_dHdx_dHdt_Index           */
+    uint8_t *converge;                    /* d_is_GPU_HC_Sol_Converge            */
+    uint8_t *infinity;                    /* d_is_GPU_HC_Sol_Infinity            */
+    hcPathStats *stats;                   /* optional, 312*N entries             */
+} hcTrackArgs;
+
+/* Extra arguments of the early-abort ("TrunRANSAC") launch. */
+typedef struct {
+    int num_triplet_edgels;               /* Num_Of_Triplet_Edgels               */
+    const float *triplet_edge_locations;  /* E x 6 floats (x1 y1 x2 y2 x3 y3)     */
+    const float *intrinsic_matrix;        /* 9 floats, row-major K               */
+    uint8_t *found_trifocal_sols;         /* 1 byte flag (caller zeroes it)      */
+    int32_t *trifocal_sols_batch_index;   /* 312*N ints (caller sets -1)         */
+} hcAbortArgs;
+
+/* Workspace: holds the compacted index tables, the path work queue and the
+   device timestamps.  Size does not depend on N.  Caller allocates (device
+   memory, 256-B aligned). */
+size_t hc_trifocal_workspace_size(void);
+
+/* GPU-HC tracking of 312*N paths (replaces ..._TrunPaths and ..._TrunPaths_Volta). */
+hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace,
+                                       size_t workspace_bytes, hcStream stream);
+
+/* GPU-HC tracking with on-device RANSAC hypothesis scoring and early abort
+   (replaces ..._TrunPaths_TrunRANSAC and ..._TrunRANSAC_Volta). */
+hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAbortArgs *abort_args,
+                                             void *workspace, size_t workspace_bytes,
+                                             hcStream stream);
+
+/* Device timestamps of the last launch on this workspace, in seconds since the
+   launch started: [0] = first good hypothesis found (abort mode, <0 if none).
+   Reads the workspace with a blocking copy -- call after synchronising. */
+hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_seconds);
+
+/* ---- component entry points (batched building blocks, also used by tests) ---- */
+
+/* Batched 30x30 complex solve with the tracker's LU (partial pivoting on
+   |re|+|im|, dev-cgesv-batched-small.cuh:38-107 semantics): A row-major n x 30 x 30,
+   b n x 30, x n x 30. */
+hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, hcComplex *x,
+                                hcStream stream);
+
+/* Batched evaluation of dH/dx (row-major 30x30), dH/dt and H at (x, p) with
+   the compacted tables built from unified_index (gpu-idx-evals/dev-eval-indxing-
+   trifocal_2op1p_30x30_LimUnroll_L2Cache.cuh:40-148).
+   x: n x 31, p: n x 34, d: n x 34.  Uses the workspace for the tables. */
+hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcComplex *x,
+                                  const hcComplex *p, const hcComplex *d, hcComplex *Hx,
+                                  hcComplex *Ht, hcComplex *H, void *workspace,
+                                  size_t workspace_bytes, hcStream stream);
+
+/* hipGetErrorString of the last HIP error seen by an entry point of this thread
+   (meaningful after an HC_ERROR_LAUNCH / HC_ERROR_DEVICE return). */
+const char *hc_last_error_string(void);
+
+/* Library / kernel identification (for logs and the bench JSON). */
+const char *hc_trifocal_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HC_TRIFOCAL_H */

@@ -1,0 +1,83 @@
+"""Generates the committed golden fixtures from the C oracle (oracle/hc_oracle.c).
+
+Inputs are the reference's own data files (copied unmodified under data/); the
+outputs pin the oracle so later rounds (and the GPU box, which has no
+/root/reference) check against fixed vectors:
+
+  samples_seed0.npz     Prepare_Target_Params(srand(0)) for 100 samples: picked edgel ids + target/diff
+  gpuhc_N100_seed0.npz  GPU-HC semantics, 100 samples: conv/inf/steps/corrections per path,
+                        a 64-bit hash of every final track, full tracks of samples 0..1,
+                        hypothesis-scoring results of every converged path
+  cpuhc_seed0.npz       CPU-HC semantics: counts for 100 samples + flags/hashes of samples 0..1
+  kat_eval.npz          one evaluation point: x, p, d -> dH/dx, dH/dt, H and the LU solve
+
+Run:  python tests/golden/make_golden.py      (takes ~1-2 min on 8 cores)
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle as O  # noqa: E402
+
+DATA = os.path.join(ROOT, "data")
+PROB = os.path.join(DATA, "problems", "trifocal_2op1p_30x30")
+RANS = os.path.join(DATA, "RANSAC_Data", "trifocal_2op1p_30x30", "Synthetic")
+
+
+def track_hash(tracks):
+    """Per-path 64-bit polynomial hash of x[0..29] with +0/-0 and NaN canonicalised."""
+    a = np.ascontiguousarray(tracks[:, :30, :], np.float32).copy()
+    a[a == 0] = 0.0
+    a[np.isnan(a)] = np.float32(np.nan)
+    w = a.reshape(a.shape[0], -1).view(np.uint32).astype(np.uint64)
+    h = np.zeros(a.shape[0], np.uint64)
+    P = np.uint64(1099511628211)
+    with np.errstate(over="ignore"):
+        for k in range(w.shape[1]):
+            h = (h * P) ^ w[:, k]
+    return h
+
+
+def main():
+    ss, sp, dhdx, dhdt = O.read_problem(PROB)
+    U = np.concatenate([dhdx, dhdt]).astype(np.int32)
+    loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", "Triplet_Edgels_000.txt"))
+    K = O.read_floats(os.path.join(RANS, "Intrinsic_Matrix.txt"), 9)
+    tgt, dif, picked = O.prepare_target_params(0, [100], loc, tan, sp)
+    np.savez_compressed(os.path.join(HERE, "samples_seed0.npz"), picked=picked, target=tgt, diff=dif)
+
+    tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
+    conv_ids = np.nonzero(conv)[0]
+    scores = np.array([O.score_hypothesis(tr[b], loc, K) for b in conv_ids], dtype=np.int64).reshape(-1, 3)
+    np.savez_compressed(os.path.join(HERE, "gpuhc_N100_seed0.npz"),
+                        conv=conv, inf=inf, steps=st["steps"].astype(np.int16),
+                        corrections=st["corrections"].astype(np.int16), hash=track_hash(tr),
+                        tracks_s01=tr[:624], counts=np.array(O.count_solutions(tr, conv, inf)),
+                        scored_ids=conv_ids.astype(np.int32), scored=scores.astype(np.int32))
+    print("gpuhc counts", O.count_solutions(tr, conv, inf), "passing", int(scores[:, 0].sum()))
+
+    trc, cc, ic, stc, secs = O.cpuhc_track(ss, sp, tgt, dif, dhdx, dhdt)
+    np.savez_compressed(os.path.join(HERE, "cpuhc_seed0.npz"),
+                        counts=np.array(O.count_solutions(trc, cc, ic)), conv_s01=cc[:624], inf_s01=ic[:624],
+                        steps_s01=stc["steps"][:624].astype(np.int16), hash_s01=track_hash(trc[:624]))
+    print("cpuhc counts", O.count_solutions(trc, cc, ic), f"{secs:.1f}s")
+
+    # one evaluation point inside a path: sample 0, track 5, t = 0.37, x = start sol perturbed
+    rng = np.random.default_rng(7)
+    x = ss[5].copy()
+    x[:30] += (rng.standard_normal((30, 2)) * 1e-2).astype(np.float32)
+    p = O.param_homotopy(0.37, sp, tgt[0])
+    A = O.eval_hx(dhdx, x, p)
+    bt = O.eval_ht(dhdt, x, p, dif[0])
+    bh = O.eval_h(dhdt, x, p)
+    sol = O.cgesv_gpu(A, bt)
+    np.savez_compressed(os.path.join(HERE, "kat_eval.npz"), x=x, p=p, d=dif[0], Hx=A, Ht=bt, H=bh, lu_x=sol)
+
+
+if __name__ == "__main__":
+    main()

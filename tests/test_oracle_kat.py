@@ -1,0 +1,216 @@
+"""Pins the C oracle against the reference's own data and committed outputs.
+
+The reference ships no tests or golden vectors, so the oracle is
+pinned by known-answer tests derived from its committed data files:
+  KAT 1  H(start_sols, start_params) == 0 (the start system is solved)
+  KAT 2  the dH/dx table is the Jacobian of the H table (finite differences)
+  KAT 3  LU solves agree with numpy (complex128)
+  KAT 4  CPU-HC counts over 100 samples match Output_Write_Files/CPU_Sols_Statistics.txt
+and by the committed golden fixtures (tests/golden/make_golden.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import same
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+# ---------- independent float64 evaluation straight from the index tables
+def _c(a):
+    return a[..., 0].astype(np.float64) + 1j * a[..., 1].astype(np.float64)
+
+
+def h64(dHdt, x, p):
+    D = dHdt.reshape(16, 6, 30)
+    out = np.zeros(30, np.complex128)
+    for j in range(16):
+        c, a, b, u, v, w = (D[j, k] for k in range(6))
+        out += c * p[a] * p[b] * x[u] * x[v] * x[w]
+    return out
+
+
+def hx64(dHdx, x, p):
+    X = dHdx.reshape(30, 8, 5, 30)  # col, term, part, row
+    A = np.zeros((30, 30), np.complex128)
+    for col in range(30):
+        for j in range(8):
+            c, a, b, u, v = (X[col, j, k] for k in range(5))
+            A[:, col] += c * p[a] * p[b] * x[u] * x[v]
+    return A
+
+
+def _text64(name):
+    from trifocal_pose_estimation_using_improved_gpuhc_amd.problem import problem_dir
+    v = np.loadtxt(os.path.join(problem_dir(), name), dtype=np.float64)
+    return v[:, 0] + 1j * v[:, 1]
+
+
+def test_kat1_start_system_is_solved(problem):
+    """float64 straight from the text files (SURVEY §4 KAT 1: max |H| ~ 6e-12)."""
+    x_all = _text64("start_sols.txt").reshape(312, 30)
+    p = np.concatenate([_text64("start_params.txt"), [1.0]])
+    worst = 0.0
+    for k in range(312):
+        x = np.concatenate([x_all[k], [1.0]])
+        worst = max(worst, np.abs(h64(problem.dHdt_index, x, p)).max())
+    assert worst < 1e-9, worst
+
+
+def test_kat1_oracle_fp32_residual(problem, oracle, samples100):
+    tgt = samples100[0]
+    p = oracle.param_homotopy(0.0, problem.start_params, tgt[0])
+    r = max(np.abs(oracle.eval_h(problem.dHdt_index, problem.start_sols[k], p)).max() for k in range(312))
+    assert r < 1e-3  # float32-parsed inputs: ~1e-7 relative to terms of magnitude ~1e3
+
+
+def test_kat2_dhdx_is_jacobian_of_h(problem):
+    rng = np.random.default_rng(0)
+    p = _c(problem.start_params)
+    for k in rng.choice(312, 6, replace=False):
+        x = _c(problem.start_sols[k])
+        A = hx64(problem.dHdx_index, x, p)
+        eps = 1e-6
+        for col in range(30):
+            xp = x.copy(); xp[col] += eps
+            xm = x.copy(); xm[col] -= eps
+            fd = (h64(problem.dHdt_index, xp, p) - h64(problem.dHdt_index, xm, p)) / (2 * eps)
+            assert np.abs(fd - A[:, col]).max() <= 1e-6 * max(1.0, np.abs(A).max())
+
+
+def test_oracle_evals_match_fp64(problem, oracle, samples100):
+    tgt, dif, _ = samples100
+    rng = np.random.default_rng(1)
+    for _ in range(8):
+        k, s = int(rng.integers(312)), int(rng.integers(100))
+        t = float(np.float32(rng.uniform()))
+        x = problem.start_sols[k].copy()
+        x[:30] += (rng.standard_normal((30, 2)) * 1e-2).astype(np.float32)
+        p = oracle.param_homotopy(t, problem.start_params, tgt[s])
+        A = _c(oracle.eval_hx(problem.dHdx_index, x, p))
+        A64 = hx64(problem.dHdx_index, _c(x), _c(p))
+        assert np.abs(A - A64).max() <= 1e-5 * np.abs(A64).max()
+        H = _c(oracle.eval_h(problem.dHdt_index, x, p))
+        assert np.abs(H - h64(problem.dHdt_index, _c(x), _c(p))).max() <= 1e-5 * max(1.0, np.abs(H).max())
+        # dH/dt = -(d/dt) H along p(t) = start + t*(target - start): central difference in t
+        d = _c(dif[s])
+        Ht = _c(oracle.eval_ht(problem.dHdt_index, x, p, dif[s]))
+        pp = _c(p)
+        fd = (h64(problem.dHdt_index, _c(x), pp + 1e-6 * d) - h64(problem.dHdt_index, _c(x), pp - 1e-6 * d)) / 2e-6
+        assert np.abs(-fd - Ht).max() <= 1e-4 * max(1.0, np.abs(fd).max())
+
+
+def test_kat3_lu_vs_numpy(problem, oracle, samples100):
+    rng = np.random.default_rng(2)
+    tgt, dif, _ = samples100
+    for i in range(16):
+        if i < 8:
+            A = rng.standard_normal((30, 30, 2)).astype(np.float32)
+            b = rng.standard_normal((30, 2)).astype(np.float32)
+        else:
+            k = int(rng.integers(312))
+            x = problem.start_sols[k]
+            p = oracle.param_homotopy(float(np.float32(rng.uniform())), problem.start_params, tgt[i])
+            A = oracle.eval_hx(problem.dHdx_index, x, p)
+            b = oracle.eval_ht(problem.dHdt_index, x, p, dif[i])
+        xr = np.linalg.solve(_c(A), _c(b))
+        cond = np.linalg.cond(_c(A))
+        tol = 1e-6 * cond * 10
+        for xo in (_c(oracle.cgesv_gpu(A, b)), _c(oracle.cgesv_lapack(A, b)[0])):
+            assert np.abs(xo - xr).max() <= tol * max(1.0, np.abs(xr).max())
+
+
+def test_lu_zero_pivot_and_ties(oracle):
+    A = np.zeros((30, 30, 2), np.float32)
+    b = np.ones((30, 2), np.float32)
+    x = oracle.cgesv_gpu(A, b)               # singular: reference semantics produce NaN, no crash
+    assert np.isnan(x).any()
+    B, info = oracle.cgesv_lapack(A, b)       # LAPACK: info > 0, B untouched
+    assert info == 1 and (B == b).all()
+    I = np.zeros((30, 30, 2), np.float32)
+    I[np.arange(30), np.arange(30), 0] = 1.0
+    assert same(oracle.cgesv_gpu(I, b), b).all()
+
+
+def test_kat4_cpuhc_counts_match_reference_outputs():
+    """Reference CPU_Sols_Statistics.txt: 11098 converged / 521 real / 6577 inf
+    (columns swapped back).  The restatement uses other FMA / LAPACK
+    kernels, so it is pinned to within 1 %."""
+    g = np.load(os.path.join(GOLDEN, "cpuhc_seed0.npz"))
+    ref = np.array([11098, 521, 6577])
+    got = g["counts"]
+    assert (np.abs(got - ref) <= 0.01 * ref).all(), got
+
+
+def test_reference_output_files_parse():
+    """The committed reference outputs read as documented (column order converged, real, inf)."""
+    root = os.path.join(os.path.dirname(GOLDEN), "golden", "reference_outputs.txt")
+    vals = [l.split() for l in open(root).read().splitlines() if l and not l.startswith("#")]
+    d = {v[0]: [float(t) for t in v[1:]] for v in vals}
+    assert d["CPU_Sols_Statistics"] == [11098, 521, 6577]
+    assert d["GPU_Sols_Statistics"] == [272, 5, 495]
+    assert d["GPU_Timings_ms"] == [149.575]
+
+
+def test_oracle_reproduces_golden_samples(problem, ransac0, oracle):
+    g = np.load(os.path.join(GOLDEN, "samples_seed0.npz"))
+    tgt, dif, picked = oracle.prepare_target_params(0, [100], ransac0.locations, ransac0.tangents,
+                                                    problem.start_params)
+    assert (picked == g["picked"]).all() and (tgt == g["target"]).all() and (dif == g["diff"]).all()
+
+
+def test_oracle_reproduces_golden_tracks(problem, oracle, samples100):
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    tgt, dif, _ = samples100
+    tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, tgt[:2], dif[:2],
+                                           problem.unified_index)
+    assert (conv == g["conv"][:624]).all() and (inf == g["inf"][:624]).all()
+    assert (st["steps"] == g["steps"][:624]).all() and (st["corrections"] == g["corrections"][:624]).all()
+    assert same(tr, g["tracks_s01"]).all()
+
+
+def test_oracle_cpuhc_reproduces_golden(problem, oracle, samples100):
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import track_hash
+    g = np.load(os.path.join(GOLDEN, "cpuhc_seed0.npz"))
+    tgt, dif, _ = samples100
+    tr, conv, inf, st, _ = oracle.cpuhc_track(problem.start_sols, problem.start_params, tgt[:2], dif[:2],
+                                              problem.dHdx_index, problem.dHdt_index)
+    assert (conv == g["conv_s01"]).all() and (inf == g["inf_s01"]).all()
+    assert (track_hash(tr) == g["hash_s01"]).all()
+
+
+def test_gpu_semantics_prune_vs_cpu(oracle, problem, samples100):
+    """GPU-HC (depth-sign pruning) tracks fewer steps than CPU-HC and never
+    converges a path with a non-positive depth at t > 0.95."""
+    tgt, dif, _ = samples100
+    trg, cg, ig, sg = oracle.gpuhc_track(problem.start_sols, problem.start_params, tgt[:1], dif[:1],
+                                         problem.unified_index)
+    trc, cc, ic, sc, _ = oracle.cpuhc_track(problem.start_sols, problem.start_params, tgt[:1], dif[:1],
+                                            problem.dHdx_index, problem.dHdt_index)
+    assert sg["steps"].sum() < sc["steps"].sum()
+    assert cg.sum() <= cc.sum()
+
+
+def test_scoring_finds_ground_truth_pose(problem, ransac0, oracle):
+    """Noiseless data: a passing hypothesis of the golden run recovers the GT
+    relative rotation R21 within ROT_RESIDUAL_TOL (definitions.hpp:14)."""
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    ids = [int(b) for b, s in zip(g["scored_ids"], g["scored"]) if s[0] == 1]
+    b = ids[0]
+    assert b < 624
+    x = g["tracks_s01"][b]
+    ok, i21, i31 = oracle.score_hypothesis(x, ransac0.locations, ransac0.K)
+    assert ok and i21 >= 0.9 * ransac0.locations.shape[0]
+    r = x[24:27, 0].astype(np.float64)
+    a, bb, c = r
+    R = np.array([[1 + a * a - (bb * bb + c * c), 2 * (a * bb - c), 2 * (a * c + bb)],
+                  [2 * (a * bb + c), 1 + bb * bb - (a * a + c * c), 2 * (bb * c - a)],
+                  [2 * (a * c - bb), 2 * (bb * c + a), 1 + c * c - (a * a + bb * bb)]])
+    R /= np.linalg.norm(R[:, 0])
+    Rgt = ransac0.pose21[:9].reshape(3, 3).astype(np.float64)
+    ang = np.arccos(np.clip((np.trace(R.T @ Rgt) - 1) / 2, -1, 1))
+    assert ang < 0.1, ang

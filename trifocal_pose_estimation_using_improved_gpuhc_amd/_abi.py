@@ -1,0 +1,102 @@
+"""ctypes binding of the C-ABI in include/hc_trifocal.h and include/hc_host.h.
+
+The native library (lib/libhc_trifocal.so, HIP for gfx950) is the product: this
+module only marshals pointers.  It raises if the library is missing -- there is
+no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libhc_trifocal.so")
+
+NUM_VARS, NUM_PARAMS, NUM_TRACKS = 30, 33, 312
+NPP = NUM_PARAMS + 1
+UNIFIED_INDEX_SIZE = 38880
+
+HC_STATUS = {0: "HC_SUCCESS", 1: "HC_ERROR_INVALID_VALUE", 2: "HC_ERROR_WORKSPACE", 3: "HC_ERROR_LAUNCH",
+             4: "HC_ERROR_DEVICE", 5: "HC_ERROR_TABLE"}
+
+
+class HCError(RuntimeError):
+    pass
+
+
+class hcTrackSettings(C.Structure):
+    _fields_ = [("max_steps", C.c_int), ("max_corrections", C.c_int), ("delta_t_inc_steps", C.c_int)]
+
+
+class hcTrackArgs(C.Structure):
+    _fields_ = [("sub_ransac_iters", C.c_int),
+                ("settings", hcTrackSettings),
+                ("start_sols", C.c_void_p),
+                ("start_sols_array", C.c_void_p),
+                ("tracks", C.c_void_p),
+                ("track_array", C.c_void_p),
+                ("start_params", C.c_void_p),
+                ("target_params", C.c_void_p),
+                ("diff_params", C.c_void_p),
+                ("unified_index", C.c_void_p),
+                ("converge", C.c_void_p),
+                ("infinity", C.c_void_p),
+                ("stats", C.c_void_p)]
+
+
+class hcAbortArgs(C.Structure):
+    _fields_ = [("num_triplet_edgels", C.c_int),
+                ("triplet_edge_locations", C.c_void_p),
+                ("intrinsic_matrix", C.c_void_p),
+                ("found_trifocal_sols", C.c_void_p),
+                ("trifocal_sols_batch_index", C.c_void_p)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load the native library (raises HCError if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise HCError(f"native library missing: {LIB_PATH} (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        L = C.CDLL(LIB_PATH)
+        L.hc_trifocal_workspace_size.restype = C.c_size_t
+        L.hc_trifocal_version.restype = C.c_char_p
+        L.hc_last_error_string.restype = C.c_char_p
+        for fn in ("hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
+                   "hc_trifocal_read_timings", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched"):
+            getattr(L, fn).restype = C.c_int
+        L.hc_trifocal_2op1p_30x30_track.argtypes = [C.POINTER(hcTrackArgs), C.c_void_p, C.c_size_t, C.c_void_p]
+        L.hc_trifocal_2op1p_30x30_track_abort.argtypes = [C.POINTER(hcTrackArgs), C.POINTER(hcAbortArgs),
+                                                          C.c_void_p, C.c_size_t, C.c_void_p]
+        L.hc_trifocal_read_timings.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        L.hc_cgesv_30x30_batched.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.hc_trifocal_eval_batched.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                               C.c_void_p]
+        L.hc_prepare_target_params.argtypes = [C.c_uint, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        for fn in ("hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
+                   "hc_count_triplet_edgels", "hc_read_triplet_edgels"):
+            getattr(L, fn).restype = C.c_int
+        _lib = L
+    return _lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        detail = lib().hc_last_error_string().decode(errors="replace")
+        raise HCError(f"{what} failed: {HC_STATUS.get(status, status)} ({detail})")
+
+
+# Exported symbols that include/*.h declare (tests check the library exports all of them).
+DECLARED_SYMBOLS = (
+    "hc_trifocal_workspace_size", "hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
+    "hc_trifocal_read_timings", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
+    "hc_last_error_string",
+    "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
+    "hc_count_triplet_edgels", "hc_read_triplet_edgels", "hc_split_samples", "hc_prepare_target_params",
+    "hc_count_solutions",
+)

@@ -1,0 +1,484 @@
+// hc_kernels.hip -- MI355X (gfx950) GPU-HC tracker kernels + the C-ABI of
+// include/hc_trifocal.h.
+//
+// Replaces magmaHC/gpu-kernels/kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths[_TrunRANSAC][_Volta].cu
+// (the four CUDA/MAGMA kernels + launchers, magmaHC-kernels.hpp:24-105).
+//
+// Design: a persistent grid of 256-thread workgroups; each of the
+// 4 wavefronts pulls path ids b = sample*312 + track from a device work queue
+// (one agent-scope atomicAdd per path) and tracks that path alone: lane r < 30
+// owns Jacobian row r, RHS r and x_r in VGPRs.  One predictor/corrector
+// "stage" = p(t) (LDS) + dH/dx + dH/dt|H from the LDS-resident compacted index
+// tables + the register LU.  Early abort (TrunRANSAC) scores converged paths
+// with all 64 lanes and raises an agent-scope flag.
+#include "hc_device.hpp"
+#include "../../include/hc_trifocal.h"
+
+#include <atomic>
+#include <mutex>
+
+namespace hc {
+
+static thread_local hipError_t g_last_hip_error = hipSuccess;
+static inline hcStatus launch_status(hcStatus on_fail) {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { g_last_hip_error = e; return on_fail; }
+    return HC_SUCCESS;
+}
+
+constexpr int WG_THREADS = 256;
+constexpr int WAVES_PER_WG = WG_THREADS / WAVE;
+
+struct KArgs {
+    int num_paths;
+    int max_steps, max_corr, inc_steps;
+    const cf *start_sols;
+    const cf *const *start_sols_array;
+    cf *tracks;
+    cf *const *track_array;
+    const cf *start_params;
+    const cf *target_params;
+    const cf *diff_params;
+    uint8_t *conv;
+    uint8_t *inf;
+    hcPathStats *stats;
+    TableWS *ws;
+    // abort mode
+    int num_edgels;
+    const float *edgels;
+    const float *K;
+    uint8_t *found_flag;
+    int32_t *batch_index;
+};
+
+// ---------------------------------------------------------------- table prep
+// Compacts the reference's padded unified index (38880 ints) into the slot
+// tables of TableWS.  One workgroup, thread r < 30 = equation row r.
+__global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ U, TableWS *ws,
+                                                    const uint8_t *found_in) {
+    __shared__ int cnt[NV][32];
+    __shared__ int s_nslot[NV], s_base[NV + 1];
+    const int r = threadIdx.x;
+    if (r < NV) {
+        for (int c = 0; c < NV; c++) {
+            int n = 0;
+            for (int j = 0; j < HX_TERMS; j++) n += U[(c * HX_TERMS + j) * HX_PARTS * NV + r] != 0;
+            cnt[c][r] = n;
+        }
+    }
+    __syncthreads();
+    if (r == 0) {
+        int base = 0;
+        for (int c = 0; c < NV; c++) {
+            int mx = 0;
+            for (int q = 0; q < NV; q++) mx = max(mx, cnt[c][q]);
+            s_nslot[c] = mx;
+            s_base[c] = base;
+            base += mx;
+        }
+        s_base[NV] = base;
+        for (int c = 0; c < NV; c++) { ws->nslot[c] = s_nslot[c]; ws->slot_base[c] = s_base[c]; }
+        ws->nslot[NV] = base;
+        if (base > HX_SLOT_CAP) ws->status = HC_ERROR_TABLE;
+        if (found_in) ws->found = found_in[0] ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool overflow = s_base[NV] > HX_SLOT_CAP;
+    if (r < 32 && !overflow) {
+        for (int c = 0; c < NV; c++) {
+            int k = 0;
+            if (r < NV) {
+                for (int j = 0; j < HX_TERMS; j++) {
+                    const int base = (c * HX_TERMS + j) * HX_PARTS * NV + r;
+                    const int co = U[base];
+                    if (co == 0) continue;
+                    const uint32_t w = (uint32_t)(co & 0xF) | ((uint32_t)U[base + NV] << 4) |
+                                       ((uint32_t)U[base + 2 * NV] << 10) | ((uint32_t)U[base + 3 * NV] << 16) |
+                                       ((uint32_t)U[base + 4 * NV] << 21);
+                    ws->hx[(s_base[c] + k) * 32 + r] = w;
+                    k++;
+                }
+            }
+            for (; k < s_nslot[c]; k++) ws->hx[(s_base[c] + k) * 32 + r] = 0u;
+        }
+        const int32_t *D = U + HX_SIZE;
+        int k = 0;
+        if (r < NV) {
+            for (int j = 0; j < HT_TERMS; j++) {
+                const int base = j * HT_PARTS * NV + r;
+                const int co = D[base];
+                if (co == 0) continue;
+                const uint32_t w = (uint32_t)(co & 0xF) | ((uint32_t)D[base + NV] << 4) | ((uint32_t)D[base + 2 * NV] << 10) |
+                                   ((uint32_t)D[base + 3 * NV] << 16) | ((uint32_t)D[base + 4 * NV] << 21) |
+                                   ((uint32_t)D[base + 5 * NV] << 26);
+                ws->ht[k * 32 + r] = w;
+                k++;
+            }
+        }
+        for (; k < HT_TERMS; k++) ws->ht[k * 32 + r] = 0u;
+    }
+}
+
+// per-workgroup LDS
+struct WaveLDS {
+    cf x[32];     // current track, x[30] = 1
+    cf p[NPP];    // p(t)
+    cf tgt[NPP];  // target params of the current sample
+    cf dif[NPP];  // diff params of the current sample
+};
+struct BlockLDS {
+    uint32_t hx[HX_SLOT_CAP * 32];
+    uint32_t ht[HT_TERMS * 32];
+    cf sp[NPP];
+    WaveLDS w[WAVES_PER_WG];
+};
+
+__device__ __forceinline__ void load_tables(BlockLDS &L, const TableWS *ws, const cf *start_params) {
+    const int S = ws->nslot[NV];
+    for (int i = threadIdx.x; i < S * 32; i += WG_THREADS) L.hx[i] = ws->hx[i];
+    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) L.ht[i] = ws->ht[i];
+    if (threadIdx.x < NPP) L.sp[threadIdx.x] = start_params[threadIdx.x];
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------- tracker
+// kernel_GPUHC_trifocal_pose_PH_CodeOpt_TrunPaths (.cu:45-290) and, with
+// ABORT, ..._TrunPaths_TrunRANSAC (.cu:45-327).
+template <bool ABORT>
+__global__ void __launch_bounds__(WG_THREADS) k_track(KArgs a) {
+    __shared__ BlockLDS L;
+    TableWS *ws = a.ws;
+    if (ws->status != 0u) return;
+    load_tables(L, ws, a.start_params);
+    if (ABORT && threadIdx.x == 0) {
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        atomicCAS(&ws->t_start, 0ull, now);
+    }
+    const int lane = lane_id();
+    const int l32 = lane & 31;
+    const int wid = threadIdx.x / WAVE;
+    WaveLDS &W = L.w[wid];
+    const int *__restrict__ g_nslot = ws->nslot;
+    const int *__restrict__ g_base = ws->slot_base;
+    if (lane == 30) W.x[30] = cmk(1.0f, 0.0f);
+    if (lane == 31) W.x[31] = cmk(0.0f, 0.0f);
+    if (lane == 33) W.p[33] = cmk(1.0f, 0.0f);
+    int cur_smp = -1;
+
+    for (;;) {
+        int b = 0;
+        if (lane == 0) b = (int)atomicAdd(&ws->queue, 1u);
+        b = uni(b);
+        if (b >= a.num_paths) break;
+        const int trk = b % NTRK, smp = b / NTRK;                          // :67-69
+        cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+        if (ABORT) {                                                       // TrunRANSAC.cu:152
+            const unsigned f = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (uni((int)f) != 0) {                                        // skipped: x stays start, conv 0
+                if (lane == 0) {
+                    a.conv[b] = 0;
+                    a.inf[b] = 0;
+                    if (a.stats) a.stats[b] = hcPathStats{0, 0, 0, 0};
+                }
+                continue;
+            }
+        }
+        if (smp != cur_smp) {                                              // :107-118
+            if (lane < NPP) {
+                W.tgt[lane] = a.target_params[(size_t)smp * NPP + lane];
+                W.dif[lane] = a.diff_params[(size_t)smp * NPP + lane];
+            }
+            cur_smp = smp;
+        }
+        const cf *dstart = a.start_sols_array ? a.start_sols_array[trk] : a.start_sols + (size_t)trk * (NV + 1);
+        const bool rl = lane < NV;
+        cf x = rl ? dtrack[lane] : cmk(0.0f, 0.0f);                      // :101-103
+        cf sols = rl ? dstart[lane] : cmk(0.0f, 0.0f);
+        cf xl = x;
+        wave_lds_sync();
+
+        float t0 = 0.0f, t_step = 0.0f, delta_t = 0.01f;                   // :80
+        bool end_zone = false, check_depths = true, isSucc = false, isInf = false;
+        int succ = 0, nsteps = 0, ncorr = 0;
+
+        for (int step = 0; step <= a.max_steps; step++) {                  // :138
+            if (!((double)t0 < 1.0 && (1.0 - (double)t0 > 0.0000001))) break;
+            if (!end_zone && (double)__builtin_fabsf(1.0f - t0) <= 0.0500001) end_zone = true;  // :144
+            if (check_depths) {                                            // :149-153
+                const unsigned long long pos = __ballot(lane < 8 && x.x > 0.0f);
+                const bool allpos = (pos & 0xFFull) == 0xFFull;
+                if (t0 > 0.0f) check_depths = !allpos;
+            }
+            if ((double)t0 > 0.95 && check_depths) break;                  // :154
+            if (end_zone) {                                                // :156-162
+                if (delta_t > __builtin_fabsf(1.0f - t0)) delta_t = __builtin_fabsf(1.0f - t0);
+            } else if ((double)delta_t > __builtin_fabs(0.95 - (double)t0)) {
+                delta_t = (float)__builtin_fabs(0.95 - (double)t0);
+            }
+            t_step = t0;
+            const float h2 = (float)(0.5 * (double)delta_t);               // :165
+            float scale = 0.0f;
+            int coef = 1;
+            nsteps++;
+            // one stage per iteration: s = 0..3 predictor (RK4), s >= 4 corrector
+            for (int s = 0;; s++) {
+                const bool pred = s < 4;
+                if (pred) {                                                // :181
+                    const float omt = (float)(1.0 - (double)t0);
+                    if (lane < NPP - 1) W.p[lane] = cadd(cscale(W.tgt[lane], t0), cscale(L.sp[lane], omt));
+                }
+                if (rl) W.x[lane] = x;
+                wave_lds_sync();
+                cf rA[NV];
+                eval_hx(rA, L.hx, g_nslot, g_base, W.x, W.p, l32);         // :184 / :220
+                const cf rB = pred ? eval_ht(L.ht, W.x, W.p, W.dif, l32)   // :185
+                                   : eval_h(L.ht, W.x, W.p, l32);          // :221
+                wave_lds_sync();
+                const cf k = lu_solve(rA, rB, lane);                       // :188 / :224
+                if (pred) {
+                    if (s < 3) {                                           // :191-205
+                        const float w = (float)((double)coef * 1.0 / 6.0);
+                        sols = cadd(sols, cscale(cscale(k, delta_t), w));
+                        if (coef > 1) x = xl;
+                        const int sc = (s == 1) ? 0 : 1;                   // scales {1,0,1}
+                        scale += (float)sc * h2;
+                        coef <<= sc;
+                        x = cadd(x, cscale(k, scale));
+                        t0 += (float)sc * h2;
+                    } else {                                               // :209-210
+                        sols = cadd(sols, cdivs(cscale(cscale(k, delta_t), 1.0f), 6.0f));
+                        x = sols;
+                    }
+                    if (a.max_corr <= 0 && s == 3) break;
+                } else {                                                   // :228-249
+                    x = csub(x, k);
+                    ncorr++;
+                    const float vs = rl ? k.x * k.x + k.y * k.y : 0.0f;
+                    const float vc = rl ? x.x * x.x + x.y * x.y : 0.0f;
+                    const float ns = tree_sum32(vs), nc = tree_sum32(vc);
+                    isSucc = (double)ns < 0.000001 * (double)nc;
+                    isInf = (double)nc > 1e14;
+                    if (isInf || isSucc || (s - 4) + 1 >= a.max_corr) break;
+                }
+            }
+            if (isInf) break;                                              // :252
+            if (!isSucc) {                                                 // :257-265
+                delta_t = (float)((double)delta_t * 0.5);
+                x = xl;
+                sols = xl;
+                succ = 0;
+                t0 = t_step;
+            } else {                                                       // :266-275
+                succ++;
+                xl = x;
+                sols = x;
+                if (succ >= a.inc_steps) { succ = 0; delta_t *= 2.0f; }
+            }
+        }
+        // write back (:282-286)
+        const bool converged = ((double)t0 >= 1.0 || (1.0 - (double)t0 <= 0.0000001));
+        if (rl) dtrack[lane] = x;
+        int2 inl = make_int2(0, 0);
+        if (ABORT && converged) {                                          // TrunRANSAC.cu:312-322
+            if (rl) W.x[lane] = x;
+            wave_lds_sync();
+            const unsigned long long im_ok =
+                __ballot(lane >= 18 && lane < NV && (double)__builtin_fabsf(x.y) < 1e-5);
+            if ((im_ok & 0x3FFC0000ull) == 0x3FFC0000ull) {                // lanes 18..29, eval.cuh:46-53
+                Hyp h;
+                make_hypothesis(W.x, h);
+                const float fx = a.K[0], fy = a.K[4], cx = a.K[3] /* eval quirk */, cy = a.K[5];
+                inl = score_hypothesis(h, a.edgels, a.num_edgels, fx, fy, cx, cy, lane);
+                const float r21 = (float)inl.x / (float)a.num_edgels;
+                const float r31 = (float)inl.y / (float)a.num_edgels;
+                if ((double)r21 >= 0.90 && (double)r31 >= 0.90 && lane == 0) {   // :241-246
+                    __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    a.found_flag[0] = 1;
+                    a.batch_index[b] = b;
+                    atomicCAS(&ws->t_found, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+                }
+            }
+            wave_lds_sync();
+        }
+        if (lane == 0) {
+            a.conv[b] = converged ? 1 : 0;
+            a.inf[b] = isInf ? 1 : 0;
+            if (a.stats) a.stats[b] = hcPathStats{nsteps, ncorr, inl.x, inl.y};
+        }
+    }
+}
+
+// ---------------------------------------------------------------- components
+__global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restrict__ A, const cf *__restrict__ B,
+                                                      cf *__restrict__ X) {
+    const int lane = lane_id();
+    const int sys = blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE;
+    if (sys >= n) return;   // wave-uniform
+    cf rA[NV];
+    const bool rl = lane < NV;
+#pragma unroll
+    for (int c = 0; c < NV; c++) rA[c] = rl ? A[((size_t)sys * NV + lane) * NV + c] : cmk(0.0f, 0.0f);
+    const cf rB = rl ? B[(size_t)sys * NV + lane] : cmk(0.0f, 0.0f);
+    const cf x = lu_solve(rA, rB, lane);
+    if (rl) X[(size_t)sys * NV + lane] = x;
+}
+
+__global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const TableWS *ws, const cf *__restrict__ X,
+                                                     const cf *__restrict__ P, const cf *__restrict__ D,
+                                                     cf *__restrict__ HX, cf *__restrict__ HT, cf *__restrict__ H) {
+    __shared__ BlockLDS L;
+    load_tables(L, ws, P);
+    const int lane = lane_id();
+    const int wid = threadIdx.x / WAVE;
+    const int sys = blockIdx.x * WAVES_PER_WG + wid;
+    if (sys >= n) return;
+    WaveLDS &W = L.w[wid];
+    if (lane < 31) W.x[lane] = X[(size_t)sys * 31 + lane];
+    if (lane == 31) W.x[31] = cmk(0.0f, 0.0f);
+    if (lane < NPP) { W.p[lane] = P[(size_t)sys * NPP + lane]; W.dif[lane] = D[(size_t)sys * NPP + lane]; }
+    wave_lds_sync();
+    cf rA[NV];
+    eval_hx(rA, L.hx, ws->nslot, ws->slot_base, W.x, W.p, lane & 31);
+    const cf ht = eval_ht(L.ht, W.x, W.p, W.dif, lane & 31);
+    const cf h = eval_h(L.ht, W.x, W.p, lane & 31);
+    if (lane < NV) {
+#pragma unroll
+        for (int c = 0; c < NV; c++) HX[((size_t)sys * NV + lane) * NV + c] = rA[c];
+        HT[(size_t)sys * NV + lane] = ht;
+        H[(size_t)sys * NV + lane] = h;
+    }
+}
+
+// ---------------------------------------------------------------- host side
+static int grid_for(int waves_needed, const void *kernel) {
+    static std::mutex mu;
+    static int cache_dev = -1, cache_blocks = 0, cache_cus = 0;
+    static const void *cache_k = nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return -1;
+    {
+        std::lock_guard<std::mutex> g(mu);
+        if (dev != cache_dev || kernel != cache_k) {
+            int cus = 0, per_cu = 0;
+            if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, WG_THREADS, 0) != hipSuccess) per_cu = 1;
+            cache_dev = dev; cache_k = kernel; cache_cus = cus; cache_blocks = per_cu < 1 ? 1 : per_cu;
+        }
+    }
+    const int want = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    const int cap = cache_cus * cache_blocks;
+    return want < cap ? want : cap;
+}
+
+static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *workspace, size_t wsb,
+                             hcStream stream, bool abort_mode) {
+    if (!t || t->sub_ransac_iters < 0) return HC_ERROR_INVALID_VALUE;
+    if (!workspace || wsb < sizeof(TableWS)) return HC_ERROR_WORKSPACE;
+    if (t->sub_ransac_iters == 0) return HC_SUCCESS;
+    if ((!t->start_sols && !t->start_sols_array) || (!t->tracks && !t->track_array) || !t->start_params ||
+        !t->target_params || !t->diff_params || !t->unified_index || !t->converge || !t->infinity)
+        return HC_ERROR_INVALID_VALUE;
+    if (t->settings.max_steps < 0 || t->settings.max_corrections < 0 || t->settings.delta_t_inc_steps < 0)
+        return HC_ERROR_INVALID_VALUE;
+    if (abort_mode && (!ab || ab->num_triplet_edgels <= 0 || !ab->triplet_edge_locations || !ab->intrinsic_matrix ||
+                       !ab->found_trifocal_sols || !ab->trifocal_sols_batch_index))
+        return HC_ERROR_INVALID_VALUE;
+    const long long paths = (long long)t->sub_ransac_iters * NTRK;
+    if (paths > 0x7FFFFFFFll) return HC_ERROR_INVALID_VALUE;
+    hipStream_t s = (hipStream_t)stream;
+    TableWS *ws = (TableWS *)workspace;
+    (void)hipGetLastError();  // errors of earlier, unrelated calls are not ours
+    if ((g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
+    hipLaunchKernelGGL(k_prep_tables, dim3(1), dim3(64), 0, s, t->unified_index, ws,
+                       abort_mode ? ab->found_trifocal_sols : nullptr);
+    if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
+    KArgs k{};
+    k.num_paths = (int)paths;
+    k.max_steps = t->settings.max_steps;
+    k.max_corr = t->settings.max_corrections;
+    k.inc_steps = t->settings.delta_t_inc_steps;
+    k.start_sols = (const cf *)t->start_sols;
+    k.start_sols_array = (const cf *const *)t->start_sols_array;
+    k.tracks = (cf *)t->tracks;
+    k.track_array = (cf *const *)t->track_array;
+    k.start_params = (const cf *)t->start_params;
+    k.target_params = (const cf *)t->target_params;
+    k.diff_params = (const cf *)t->diff_params;
+    k.conv = t->converge;
+    k.inf = t->infinity;
+    k.stats = t->stats;
+    k.ws = ws;
+    const void *kern = abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>;
+    const int grid = grid_for((int)paths, kern);
+    if (grid <= 0) return HC_ERROR_DEVICE;
+    if (abort_mode) {
+        k.num_edgels = ab->num_triplet_edgels;
+        k.edgels = ab->triplet_edge_locations;
+        k.K = ab->intrinsic_matrix;
+        k.found_flag = ab->found_trifocal_sols;
+        k.batch_index = ab->trifocal_sols_batch_index;
+        hipLaunchKernelGGL(k_track<true>, dim3(grid), dim3(WG_THREADS), 0, s, k);
+    } else {
+        hipLaunchKernelGGL(k_track<false>, dim3(grid), dim3(WG_THREADS), 0, s, k);
+    }
+    return launch_status(HC_ERROR_LAUNCH);
+}
+
+}  // namespace hc
+
+extern "C" {
+
+size_t hc_trifocal_workspace_size(void) { return (sizeof(hc::TableWS) + 255) & ~(size_t)255; }
+
+hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,
+                                       hcStream stream) {
+    return hc::launch_track(args, nullptr, workspace, workspace_bytes, stream, false);
+}
+
+hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAbortArgs *abort_args,
+                                             void *workspace, size_t workspace_bytes, hcStream stream) {
+    return hc::launch_track(args, abort_args, workspace, workspace_bytes, stream, true);
+}
+
+hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_seconds) {
+    if (!workspace || !first_found_seconds) return HC_ERROR_INVALID_VALUE;
+    hc::TableWS h;
+    if (hipMemcpy(&h, workspace, 64, hipMemcpyDeviceToHost) != hipSuccess) return HC_ERROR_DEVICE;
+    // s_memrealtime ticks at a constant 100 MHz on gfx9 parts
+    *first_found_seconds = (h.t_found && h.t_start) ? (double)(long long)(h.t_found - h.t_start) / 100.0e6 : -1.0;
+    return HC_SUCCESS;
+}
+
+hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, hcComplex *x, hcStream stream) {
+    if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
+    if (n == 0) return HC_SUCCESS;
+    const int grid = (n + hc::WAVES_PER_WG - 1) / hc::WAVES_PER_WG;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(hc::k_cgesv, dim3(grid), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n, (const hc::cf *)A,
+                       (const hc::cf *)b, (hc::cf *)x);
+    return hc::launch_status(HC_ERROR_LAUNCH);
+}
+
+hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcComplex *x, const hcComplex *p,
+                                  const hcComplex *d, hcComplex *Hx, hcComplex *Ht, hcComplex *H, void *workspace,
+                                  size_t workspace_bytes, hcStream stream) {
+    if (n < 0 || !unified_index || (n > 0 && (!x || !p || !d || !Hx || !Ht || !H))) return HC_ERROR_INVALID_VALUE;
+    if (!workspace || workspace_bytes < sizeof(hc::TableWS)) return HC_ERROR_WORKSPACE;
+    if (n == 0) return HC_SUCCESS;
+    hipStream_t s = (hipStream_t)stream;
+    hc::TableWS *ws = (hc::TableWS *)workspace;
+    (void)hipGetLastError();
+    if ((hc::g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
+    hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(64), 0, s, unified_index, ws, nullptr);
+    if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
+    const int grid = (n + hc::WAVES_PER_WG - 1) / hc::WAVES_PER_WG;
+    hipLaunchKernelGGL(hc::k_eval, dim3(grid), dim3(hc::WG_THREADS), 0, s, n, ws, (const hc::cf *)x,
+                       (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht, (hc::cf *)H);
+    return hc::launch_status(HC_ERROR_LAUNCH);
+}
+
+const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
+
+const char *hc_trifocal_version(void) { return "hc_trifocal gfx950 v1 (wave-per-path, register LU)"; }
+
+}  // extern "C"
