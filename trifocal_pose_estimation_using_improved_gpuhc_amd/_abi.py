@@ -61,6 +61,10 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise HCError(f"native library missing: {LIB_PATH} (run `python -c 'import __graft_entry__ as g; g.build()'`)")
+        # torch is the process' HIP runtime owner (device memory, streams):
+        # load it first so libhc_trifocal.so binds to the same libamdhip64.so.7
+        # instead of pulling a second HIP/HSA runtime from /opt/rocm.
+        import torch  # noqa: F401
         L = C.CDLL(LIB_PATH)
         L.hc_trifocal_workspace_size.restype = C.c_size_t
         L.hc_trifocal_version.restype = C.c_char_p

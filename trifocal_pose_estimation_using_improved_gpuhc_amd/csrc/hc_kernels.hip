@@ -12,9 +12,11 @@
 // tables + the register LU.  Early abort (TrunRANSAC) scores converged paths
 // with all 64 lanes and raises an agent-scope flag.
 #include "hc_device.hpp"
+#include "hc_track2.hpp"
 #include "../../include/hc_trifocal.h"
 
 #include <atomic>
+#include <cstdlib>
 #include <mutex>
 
 namespace hc {
@@ -43,6 +45,7 @@ struct KArgs {
     uint8_t *inf;
     hcPathStats *stats;
     TableWS *ws;
+    TableWS2 *ws2;
     // abort mode
     int num_edgels;
     const float *edgels;
@@ -117,6 +120,53 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
         }
         for (; k < HT_TERMS; k++) ws->ht[k * 32 + r] = 0u;
     }
+    // ---- v2: per-lane dH/dx term lists + column -> entry-slot map
+    __shared__ int s_len[32];
+    TableWS2 *w2 = (TableWS2 *)((char *)ws + ((sizeof(TableWS) + 255) & ~(size_t)255));
+    if (r < 32) {
+        int n = 0, slot = 0;
+        uint32_t map[3] = {0u, 0u, 0u};
+        for (int c = 0; c < NV; c++) map[c / 10] |= 6u << (3 * (c % 10));
+        if (r < NV) {
+            for (int c = 0; c < NV; c++) {
+                int last_j = -1;
+                for (int j = 0; j < HX_TERMS; j++)
+                    if (U[(c * HX_TERMS + j) * HX_PARTS * NV + r] != 0) last_j = j;
+                if (last_j < 0) continue;
+                for (int j = 0; j <= last_j; j++) {
+                    const int base = (c * HX_TERMS + j) * HX_PARTS * NV + r;
+                    const int co = U[base];
+                    if (co == 0) continue;
+                    if (n < HX2_SLOT_CAP && slot < 6)
+                        w2->hx[n * 32 + r] = (uint32_t)(co & 0xF) | ((uint32_t)U[base + NV] << 4) |
+                                             ((uint32_t)U[base + 2 * NV] << 10) | ((uint32_t)U[base + 3 * NV] << 16) |
+                                             ((uint32_t)U[base + 4 * NV] << 21) | ((uint32_t)slot << 26) |
+                                             ((uint32_t)(j == last_j) << 29);
+                    n++;
+                }
+                map[c / 10] = (map[c / 10] & ~(7u << (3 * (c % 10)))) | ((uint32_t)slot << (3 * (c % 10)));
+                slot++;
+            }
+        }
+        for (int q = 0; q < 3; q++) w2->map[q][r] = map[q];
+        s_len[r] = (slot > 6) ? (1 << 20) : n;
+    }
+    __syncthreads();
+    if (r == 0) {
+        int mx = 0;
+        for (int q = 0; q < 32; q++) mx = max(mx, s_len[q]);
+        w2->hx_len = mx;
+        w2->status = (mx > HX2_SLOT_CAP) ? HC_ERROR_TABLE : 0;
+    }
+    __syncthreads();
+    if (r < 32) {
+        const int len = min(w2->hx_len, HX2_SLOT_CAP);
+        for (int k2 = s_len[r]; k2 < len; k2++) w2->hx[k2 * 32 + r] = 0u;
+    }
+}
+
+__host__ __device__ __forceinline__ TableWS2 *ws2_of(TableWS *ws) {
+    return (TableWS2 *)((char *)ws + ((sizeof(TableWS) + 255) & ~(size_t)255));
 }
 
 // per-workgroup LDS
@@ -308,6 +358,297 @@ __global__ void __launch_bounds__(WG_THREADS) k_track(KArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- tracker v2
+// Two paths per wavefront (hc_track2.hpp).  Each half-wave is a path slot with
+// its own stage machine; one loop iteration runs one stage (p(t), dH/dx,
+// dH/dt|H, LU) for both slots.  Phases of a slot:
+enum : int { PH_DEQ = 0, PH_BEGIN = 1, PH_STAGE = 2, PH_FINISH = 3, PH_IDLE = 4 };
+
+__device__ __forceinline__ int half_sum_i(int v) {
+    v += dpp_i<DPP_QP_1032>(v);
+    v += dpp_i<DPP_QP_2301>(v);
+    v += dpp_i<DPP_ROW_HALF_MIRROR>(v);
+    v += dpp_i<DPP_ROW_MIRROR>(v);
+    v += swz_xor16_i(v);
+    return v;
+}
+
+template <bool ABORT, int MINW>
+__global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
+    __shared__ uint32_t s_hx2[HX2_SLOT_CAP * 32];
+    __shared__ uint32_t s_ht[HT_TERMS * 32];
+    __shared__ cf s_sp[NPP];
+    __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
+    TableWS *ws = a.ws;
+    TableWS2 *w2 = a.ws2;
+    if ((ws->status | (unsigned)w2->status) != 0u) return;
+    const int hx_len = w2->hx_len;
+    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx2[i] = w2->hx[i];
+    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht[i] = ws->ht[i];
+    if (threadIdx.x < NPP) s_sp[threadIdx.x] = a.start_params[threadIdx.x];
+    {
+        float *z = reinterpret_cast<float *>(s_slot);
+        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
+    }
+    __syncthreads();
+    if (ABORT && threadIdx.x == 0) atomicCAS(&ws->t_start, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    const int lane = lane_id();
+    const int r = lane & 31, hb = lane & 32;
+    const int wid = threadIdx.x / WAVE;
+    SlotLDS &S = s_slot[wid * 2 + (hb >> 5)];
+    if (r == 30) S.x[30] = cmk(1.0f, 0.0f);
+    if (r == 0) S.p[33] = cmk(1.0f, 0.0f);
+    const uint32_t map[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
+    const bool rl = r < NV;
+    wave_lds_sync();
+
+    // per-slot state (uniform within a half)
+    int ph = PH_DEQ, b = -1, smp_loaded = -1;
+    int s = 0, stepidx = 0, coef = 1, succ = 0, nsteps = 0, ncorr = 0;
+    float t0 = 0.0f, t_step = 0.0f, dt = 0.01f, h2 = 0.0f, scale = 0.0f;
+    bool end_zone = false, check = true, isSucc = false, isInf = false;
+    cf x = cmk(0.0f, 0.0f), xl = x, sols = x;
+
+    for (;;) {
+        // ---------------- resolve slot phases until every slot is at a stage or idle
+        for (;;) {
+            if (ph == PH_FINISH) {                                            // :282-286
+                const bool conv = ((double)t0 >= 1.0 || (1.0 - (double)t0 <= 0.0000001));
+                cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+                if (rl) dtrack[r] = x;
+                int in21 = 0, in31 = 0;
+                if (ABORT && conv) {                                          // TrunRANSAC.cu:312-322
+                    if (rl) S.x[r] = x;
+                    wave_lds_sync();
+                    const unsigned long long im = __ballot(r >= 18 && rl && (double)__builtin_fabsf(x.y) < 1e-5);
+                    if (((unsigned)(im >> hb) & 0x3FFC0000u) == 0x3FFC0000u) {   // eval.cuh:46-53
+                        Hyp hy;
+                        make_hypothesis(S.x, hy);
+                        const float fx = a.K[0], fy = a.K[4], cx = a.K[3] /* eval quirk */, cy = a.K[5];
+                        const float *R = hy.R;
+                        const float d18 = hy.T[0], d19 = hy.T[1], d20 = hy.T[2], d21 = hy.T[3], d22 = hy.T[4], d23 = hy.T[5];
+                        int c21 = 0, c31 = 0;
+                        for (int e = r; e < a.num_edgels; e += 32) {
+                            const float *g = a.edgels + (size_t)e * 6;
+                            const float g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4], g5 = g[5];
+                            float num, den, v0, v1, v2, ex, ey;
+                            num = d20 * (R[2] * g2 + R[5] * g3 + R[8]) - (R[2] * d18 + R[5] * d19 + R[8] * d20);
+                            den = 1.0f - (R[6] * g0 + R[7] * g1 + R[8]) * (R[2] * g2 + R[5] * g3 + R[8]);
+                            v2 = num * (R[6] * g0 + R[7] * g1 + R[8]) + den * d20;
+                            v0 = (num * (R[0] * g0 + R[1] * g1 + R[2]) + den * d18) / v2;
+                            v1 = (num * (R[3] * g0 + R[4] * g1 + R[5]) + den * d19) / v2;
+                            ex = (v0 * fx + cx) - (g2 * fx + cx);
+                            ey = (v1 * fy + cy) - (g3 * fy + cy);
+                            c21 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+                            num = d23 * (R[11] * g4 + R[14] * g5 + R[17]) - (R[11] * d21 + R[14] * d22 + R[17] * d23);
+                            den = 1.0f - (R[15] * g0 + R[16] * g1 + R[17]) * (R[11] * g4 + R[14] * g5 + R[17]);
+                            v2 = num * (R[15] * g0 + R[16] * g1 + R[17]) + den * d23;
+                            v0 = (num * (R[9] * g0 + R[10] * g1 + R[11]) + den * d21) / v2;
+                            v1 = (num * (R[12] * g0 + R[13] * g1 + R[14]) + den * d22) / v2;
+                            ex = (v0 * fx + cx) - (g4 * fx + cx);
+                            ey = (v1 * fy + cy) - (g5 * fy + cy);
+                            c31 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+                        }
+                        in21 = half_sum_i(c21);
+                        in31 = half_sum_i(c31);
+                        const float r21 = (float)in21 / (float)a.num_edgels, r31 = (float)in31 / (float)a.num_edgels;
+                        if ((double)r21 >= 0.90 && (double)r31 >= 0.90 && r == 0) {   // eval.cuh:241-246
+                            __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            a.found_flag[0] = 1;
+                            a.batch_index[b] = b;
+                            atomicCAS(&ws->t_found, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+                        }
+                    }
+                }
+                if (r == 0) {
+                    a.conv[b] = conv ? 1 : 0;
+                    a.inf[b] = isInf ? 1 : 0;
+                    if (a.stats) a.stats[b] = hcPathStats{nsteps, ncorr, in21, in31};
+                }
+                ph = PH_DEQ;
+            }
+            if (ph == PH_DEQ) {
+                int nb = 0;
+                if (r == 0) nb = (int)atomicAdd(&ws->queue, 1u);
+                nb = bperm_i(nb, hb);
+                if (nb >= a.num_paths) {
+                    ph = PH_IDLE;
+                    b = -1;
+                } else {
+                    b = nb;
+                    bool skip = false;
+                    if (ABORT) {                                              // TrunRANSAC.cu:152
+                        skip = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                        skip = bperm_i((int)skip, hb) != 0;
+                        if (skip && r == 0) {
+                            a.conv[b] = 0;
+                            a.inf[b] = 0;
+                            if (a.stats) a.stats[b] = hcPathStats{0, 0, 0, 0};
+                        }
+                    }
+                    if (!skip) {
+                        const int trk = b % NTRK, smp = b / NTRK;            // :67-69
+                        if (smp != smp_loaded && r < NPP) {
+                            S.tgt[r] = a.target_params[(size_t)smp * NPP + r];
+                            S.dif[r] = a.diff_params[(size_t)smp * NPP + r];
+                        }
+                        if (smp != smp_loaded && r < NPP - 32) {
+                            S.tgt[r + 32] = a.target_params[(size_t)smp * NPP + r + 32];
+                            S.dif[r + 32] = a.diff_params[(size_t)smp * NPP + r + 32];
+                        }
+                        smp_loaded = smp;
+                        const cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+                        const cf *dstart = a.start_sols_array ? a.start_sols_array[trk]
+                                                              : a.start_sols + (size_t)trk * (NV + 1);
+                        x = rl ? dtrack[r] : cmk(0.0f, 0.0f);                 // :101-103
+                        sols = rl ? dstart[r] : cmk(0.0f, 0.0f);
+                        xl = x;
+                        t0 = 0.0f; t_step = 0.0f; dt = 0.01f;                 // :80
+                        end_zone = false; check = true; isSucc = false; isInf = false;
+                        succ = 0; nsteps = 0; ncorr = 0; stepidx = 0;
+                        ph = PH_BEGIN;
+                    }
+                }
+            }
+            if (ph == PH_BEGIN) {                                             // :138-165
+                bool done = stepidx > a.max_steps;
+                if (!done) done = !((double)t0 < 1.0 && (1.0 - (double)t0 > 0.0000001));
+                if (!done) {
+                    if (!end_zone && (double)__builtin_fabsf(1.0f - t0) <= 0.0500001) end_zone = true;
+                    if (check) {
+                        const unsigned long long pos = __ballot(r < 8 && x.x > 0.0f);
+                        const bool allpos = ((unsigned)(pos >> hb) & 0xFFu) == 0xFFu;
+                        if (t0 > 0.0f) check = !allpos;
+                    }
+                    done = (double)t0 > 0.95 && check;
+                }
+                if (!done) {
+                    if (end_zone) {
+                        if (dt > __builtin_fabsf(1.0f - t0)) dt = __builtin_fabsf(1.0f - t0);
+                    } else if ((double)dt > __builtin_fabs(0.95 - (double)t0)) {
+                        dt = (float)__builtin_fabs(0.95 - (double)t0);
+                    }
+                    t_step = t0;
+                    h2 = (float)(0.5 * (double)dt);
+                    scale = 0.0f;
+                    coef = 1;
+                    s = 0;
+                    nsteps++;
+                }
+                ph = done ? PH_FINISH : PH_STAGE;
+            }
+            if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
+        }
+        if (__ballot(ph == PH_STAGE) == 0ull) break;
+
+        // ---------------- one stage for both slots
+        // park the slot state in LDS so it does not occupy VGPRs across eval + LU
+        if (r == 0) {
+            SlotState q;
+            q.t0 = t0; q.t_step = t_step; q.dt = dt; q.h2 = h2; q.scale = scale;
+            q.s = s; q.stepidx = stepidx; q.coef = coef; q.succ = succ; q.nsteps = nsteps; q.ncorr = ncorr;
+            q.b = b; q.smp = smp_loaded; q.ph = ph;
+            q.flags = (end_zone ? 1 : 0) | (check ? 2 : 0) | (isSucc ? 4 : 0) | (isInf ? 8 : 0);
+            q.pad = 0;
+            S.st = q;
+        }
+        if (rl) { S.x[r] = x; S.xl[r] = xl; S.sols[r] = sols; }
+        {
+            const bool act0 = ph == PH_STAGE;
+            const bool pred0 = act0 && s < 4;
+            if (pred0 && r < NPP - 1) {                                      // :181 p(t), i < 33
+                const float omt = (float)(1.0 - (double)t0);
+                S.p[r] = cadd(cscale(S.tgt[r], t0), cscale(s_sp[r], omt));
+            }
+            if (pred0 && r == 0) S.p[32] = cadd(cscale(S.tgt[32], t0), cscale(s_sp[32], (float)(1.0 - (double)t0)));
+        }
+        wave_lds_sync();
+        const int s_in = s, ph_in = ph;
+        asm volatile("" :: "v"(s_in), "v"(ph_in));
+        // opaque lane id: keeps LICM from hoisting ~30 lane-derived per-pivot
+        // constants (bpermute addresses, r == i masks) out of the path loop
+        int lane_v = lane;
+        asm volatile("" : "+v"(lane_v));
+        const int r_v = lane_v & 31;
+        const bool act = ph_in == PH_STAGE;
+        const bool pred = act && s_in < 4;
+        cf rA[NV];
+        eval_hx2(rA, s_hx2, hx_len, map, S, r_v);                            // :184 / :220
+        cf rB = cmk(0.0f, 0.0f);
+        if (__ballot(pred) != 0ull) {                                        // :185
+            const cf t = eval_ht2(s_ht, S, r_v);
+            if (pred) rB = t;
+        }
+        if (__ballot(act && !pred) != 0ull) {                                // :221
+            const cf t = eval_h2(s_ht, S, r_v);
+            if (!pred) rB = t;
+        }
+        wave_lds_sync();
+        const cf k = lu_solve2(rA, rB, lane_v);                              // :188 / :224
+        wave_lds_sync();
+        {
+            const SlotState q = S.st;
+            t0 = q.t0; t_step = q.t_step; dt = q.dt; h2 = q.h2; scale = q.scale;
+            s = q.s; stepidx = q.stepidx; coef = q.coef; succ = q.succ; nsteps = q.nsteps; ncorr = q.ncorr;
+            b = q.b; smp_loaded = q.smp; ph = q.ph;
+            end_zone = q.flags & 1; check = q.flags & 2; isSucc = q.flags & 4; isInf = q.flags & 8;
+            x = rl ? S.x[r] : cmk(0.0f, 0.0f);
+            xl = rl ? S.xl[r] : cmk(0.0f, 0.0f);
+            sols = rl ? S.sols[r] : cmk(0.0f, 0.0f);
+        }
+        if (act) {
+            bool step_end = false;
+            if (pred) {
+                if (s < 3) {                                                 // :191-205
+                    const float w = (float)((double)coef * 1.0 / 6.0);
+                    sols = cadd(sols, cscale(cscale(k, dt), w));
+                    if (coef > 1) x = xl;
+                    const int sc = (s == 1) ? 0 : 1;
+                    scale += (float)sc * h2;
+                    coef <<= sc;
+                    x = cadd(x, cscale(k, scale));
+                    t0 += (float)sc * h2;
+                } else {                                                     // :209-210
+                    sols = cadd(sols, cdivs(cscale(cscale(k, dt), 1.0f), 6.0f));
+                    x = sols;
+                }
+                s++;
+                if (s == 4 && a.max_corr <= 0) step_end = true;
+            } else {                                                         // :228-249
+                x = csub(x, k);
+                ncorr++;
+                const float vs = rl ? k.x * k.x + k.y * k.y : 0.0f;
+                const float vc = rl ? x.x * x.x + x.y * x.y : 0.0f;
+                const float ns = tree_sum_half(vs), nc = tree_sum_half(vc);
+                isSucc = (double)ns < 0.000001 * (double)nc;
+                isInf = (double)nc > 1e14;
+                if (isInf || isSucc || (s - 4) + 1 >= a.max_corr) step_end = true;
+                else s++;
+            }
+            if (step_end) {
+                if (isInf) {                                                 // :252
+                    ph = PH_FINISH;
+                } else {
+                    if (!isSucc) {                                           // :257-265
+                        dt = (float)((double)dt * 0.5);
+                        x = xl;
+                        sols = xl;
+                        succ = 0;
+                        t0 = t_step;
+                    } else {                                                 // :266-275
+                        succ++;
+                        xl = x;
+                        sols = x;
+                        if (succ >= a.inc_steps) { succ = 0; dt *= 2.0f; }
+                    }
+                    stepidx++;
+                    ph = PH_BEGIN;
+                }
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- components
 __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restrict__ A, const cf *__restrict__ B,
                                                       cf *__restrict__ X) {
@@ -349,7 +690,85 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const TableWS *ws, c
     }
 }
 
+__global__ void __launch_bounds__(WG_THREADS) k_cgesv2(int n, const cf *__restrict__ A, const cf *__restrict__ B,
+                                                       cf *__restrict__ X) {
+    const int lane = lane_id();
+    const int r = lane & 31;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 2 + (lane >> 5);
+    const bool ok = sys < n && r < NV;
+    cf rA[NV];
+#pragma unroll
+    for (int c = 0; c < NV; c++) rA[c] = ok ? A[((size_t)sys * NV + r) * NV + c] : cmk(0.0f, 0.0f);
+    const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
+    const cf x = lu_solve2(rA, rB, lane);
+    if (ok) X[(size_t)sys * NV + r] = x;
+}
+
+__global__ void __launch_bounds__(WG_THREADS) k_eval2(int n, TableWS *ws, const cf *__restrict__ X,
+                                                      const cf *__restrict__ P, const cf *__restrict__ D,
+                                                      cf *__restrict__ HX, cf *__restrict__ HT, cf *__restrict__ H) {
+    __shared__ uint32_t s_hx2[HX2_SLOT_CAP * 32];
+    __shared__ uint32_t s_ht[HT_TERMS * 32];
+    __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
+    const TableWS2 *w2 = ws2_of(ws);
+    const int hx_len = w2->hx_len;
+    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx2[i] = w2->hx[i];
+    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht[i] = ws->ht[i];
+    {
+        float *z = reinterpret_cast<float *>(s_slot);
+        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
+    }
+    __syncthreads();
+    const int lane = lane_id();
+    const int r = lane & 31;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 2 + (lane >> 5);
+    SlotLDS &S = s_slot[(threadIdx.x / WAVE) * 2 + (lane >> 5)];
+    const bool ok = sys < n;
+    if (ok && r < 31) S.x[r] = X[(size_t)sys * 31 + r];
+    if (ok) {
+        S.p[r] = P[(size_t)sys * NPP + r];
+        S.dif[r] = D[(size_t)sys * NPP + r];
+        if (r < NPP - 32) { S.p[r + 32] = P[(size_t)sys * NPP + r + 32]; S.dif[r + 32] = D[(size_t)sys * NPP + r + 32]; }
+    }
+    const uint32_t map[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
+    wave_lds_sync();
+    cf rA[NV];
+    eval_hx2(rA, s_hx2, hx_len, map, S, r);
+    const cf ht = eval_ht2(s_ht, S, r);
+    const cf h = eval_h2(s_ht, S, r);
+    if (ok && r < NV) {
+#pragma unroll
+        for (int c = 0; c < NV; c++) HX[((size_t)sys * NV + r) * NV + c] = rA[c];
+        HT[(size_t)sys * NV + r] = ht;
+        H[(size_t)sys * NV + r] = h;
+    }
+}
+
 // ---------------------------------------------------------------- host side
+// HC_TRIFOCAL_KERNEL=v1 selects the one-path-per-wave kernels (A/B baseline);
+// default: v2 (two paths per wave).
+static int kernel_version() {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("HC_TRIFOCAL_KERNEL");
+        v = (e && e[0] == 'v' && e[1] == '1') ? 1 : 2;
+    }
+    return v;
+}
+// HC_TRIFOCAL_MINWAVES=2|3: register budget of the v2 tracker (waves per SIMD);
+// 3 (<= 168 VGPRs, measured 12 % faster than 2) is the default
+static int v2_minwaves() {
+    static int w = -1;
+    if (w < 0) {
+        const char *e = getenv("HC_TRIFOCAL_MINWAVES");
+        w = (e && e[0] == '2') ? 2 : 3;
+    }
+    return w;
+}
+static size_t ws_bytes_needed() {
+    return ((sizeof(TableWS) + 255) & ~(size_t)255) + ((sizeof(TableWS2) + 255) & ~(size_t)255);
+}
+
 static int grid_for(int waves_needed, const void *kernel) {
     static std::mutex mu;
     static int cache_dev = -1, cache_blocks = 0, cache_cus = 0;
@@ -373,7 +792,7 @@ static int grid_for(int waves_needed, const void *kernel) {
 static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *workspace, size_t wsb,
                              hcStream stream, bool abort_mode) {
     if (!t || t->sub_ransac_iters < 0) return HC_ERROR_INVALID_VALUE;
-    if (!workspace || wsb < sizeof(TableWS)) return HC_ERROR_WORKSPACE;
+    if (!workspace || wsb < ws_bytes_needed()) return HC_ERROR_WORKSPACE;
     if (t->sub_ransac_iters == 0) return HC_SUCCESS;
     if ((!t->start_sols && !t->start_sols_array) || (!t->tracks && !t->track_array) || !t->start_params ||
         !t->target_params || !t->diff_params || !t->unified_index || !t->converge || !t->infinity)
@@ -408,8 +827,13 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.inf = t->infinity;
     k.stats = t->stats;
     k.ws = ws;
-    const void *kern = abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>;
-    const int grid = grid_for((int)paths, kern);
+    k.ws2 = ws2_of(ws);
+    const bool v2 = kernel_version() == 2;
+    const bool w3 = v2_minwaves() == 3;
+    const void *kern = v2 ? (abort_mode ? (w3 ? (const void *)k_track2<true, 3> : (const void *)k_track2<true, 2>)
+                                        : (w3 ? (const void *)k_track2<false, 3> : (const void *)k_track2<false, 2>))
+                          : (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>);
+    const int grid = grid_for(v2 ? (int)((paths + 1) / 2) : (int)paths, kern);
     if (grid <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
         k.num_edgels = ab->num_triplet_edgels;
@@ -417,9 +841,13 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
         k.K = ab->intrinsic_matrix;
         k.found_flag = ab->found_trifocal_sols;
         k.batch_index = ab->trifocal_sols_batch_index;
-        hipLaunchKernelGGL(k_track<true>, dim3(grid), dim3(WG_THREADS), 0, s, k);
+        if (v2 && w3) hipLaunchKernelGGL((k_track2<true, 3>), dim3(grid), dim3(WG_THREADS), 0, s, k);
+        else if (v2) hipLaunchKernelGGL((k_track2<true, 2>), dim3(grid), dim3(WG_THREADS), 0, s, k);
+        else hipLaunchKernelGGL(k_track<true>, dim3(grid), dim3(WG_THREADS), 0, s, k);
     } else {
-        hipLaunchKernelGGL(k_track<false>, dim3(grid), dim3(WG_THREADS), 0, s, k);
+        if (v2 && w3) hipLaunchKernelGGL((k_track2<false, 3>), dim3(grid), dim3(WG_THREADS), 0, s, k);
+        else if (v2) hipLaunchKernelGGL((k_track2<false, 2>), dim3(grid), dim3(WG_THREADS), 0, s, k);
+        else hipLaunchKernelGGL(k_track<false>, dim3(grid), dim3(WG_THREADS), 0, s, k);
     }
     return launch_status(HC_ERROR_LAUNCH);
 }
@@ -428,7 +856,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
 
 extern "C" {
 
-size_t hc_trifocal_workspace_size(void) { return (sizeof(hc::TableWS) + 255) & ~(size_t)255; }
+size_t hc_trifocal_workspace_size(void) { return hc::ws_bytes_needed(); }
 
 hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,
                                        hcStream stream) {
@@ -452,10 +880,16 @@ hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_sec
 hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, hcComplex *x, hcStream stream) {
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
-    const int grid = (n + hc::WAVES_PER_WG - 1) / hc::WAVES_PER_WG;
     (void)hipGetLastError();
-    hipLaunchKernelGGL(hc::k_cgesv, dim3(grid), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n, (const hc::cf *)A,
-                       (const hc::cf *)b, (hc::cf *)x);
+    if (hc::kernel_version() == 2) {
+        const int per = 2 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_cgesv2, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+                           (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+    } else {
+        const int grid = (n + hc::WAVES_PER_WG - 1) / hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_cgesv, dim3(grid), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+                           (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+    }
     return hc::launch_status(HC_ERROR_LAUNCH);
 }
 
@@ -463,7 +897,7 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
                                   const hcComplex *d, hcComplex *Hx, hcComplex *Ht, hcComplex *H, void *workspace,
                                   size_t workspace_bytes, hcStream stream) {
     if (n < 0 || !unified_index || (n > 0 && (!x || !p || !d || !Hx || !Ht || !H))) return HC_ERROR_INVALID_VALUE;
-    if (!workspace || workspace_bytes < sizeof(hc::TableWS)) return HC_ERROR_WORKSPACE;
+    if (!workspace || workspace_bytes < hc::ws_bytes_needed()) return HC_ERROR_WORKSPACE;
     if (n == 0) return HC_SUCCESS;
     hipStream_t s = (hipStream_t)stream;
     hc::TableWS *ws = (hc::TableWS *)workspace;
@@ -471,14 +905,24 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
     if ((hc::g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
     hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(64), 0, s, unified_index, ws, nullptr);
     if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-    const int grid = (n + hc::WAVES_PER_WG - 1) / hc::WAVES_PER_WG;
-    hipLaunchKernelGGL(hc::k_eval, dim3(grid), dim3(hc::WG_THREADS), 0, s, n, ws, (const hc::cf *)x,
-                       (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht, (hc::cf *)H);
+    if (hc::kernel_version() == 2) {
+        const int per = 2 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_eval2, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
+                           (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
+                           (hc::cf *)H);
+    } else {
+        const int grid = (n + hc::WAVES_PER_WG - 1) / hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_eval, dim3(grid), dim3(hc::WG_THREADS), 0, s, n, ws, (const hc::cf *)x,
+                           (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht, (hc::cf *)H);
+    }
     return hc::launch_status(HC_ERROR_LAUNCH);
 }
 
 const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
 
-const char *hc_trifocal_version(void) { return "hc_trifocal gfx950 v1 (wave-per-path, register LU)"; }
+const char *hc_trifocal_version(void) {
+    return hc::kernel_version() == 2 ? "hc_trifocal gfx950 v2 (2 paths/wave, register LU, per-lane term lists)"
+                                     : "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
+}
 
 }  // extern "C"
