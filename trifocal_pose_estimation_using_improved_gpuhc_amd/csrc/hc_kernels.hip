@@ -12,7 +12,7 @@
 // tables + the register LU.  Early abort (TrunRANSAC) scores converged paths
 // with all 64 lanes and raises an agent-scope flag.
 #include "hc_device.hpp"
-#include "hc_track2.hpp"
+#include "hc_lu3.hpp"
 #include "../../include/hc_trifocal.h"
 
 #include <atomic>
@@ -373,7 +373,7 @@ __device__ __forceinline__ int half_sum_i(int v) {
     return v;
 }
 
-template <bool ABORT, int MINW>
+template <bool ABORT, int MINW, int LUV>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     __shared__ uint32_t s_hx2[HX2_SLOT_CAP * 32];
     __shared__ uint32_t s_ht[HT_TERMS * 32];
@@ -584,7 +584,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
             if (!pred) rB = t;
         }
         wave_lds_sync();
-        const cf k = lu_solve2(rA, rB, lane_v);                              // :188 / :224
+        cf k;                                                                // :188 / :224
+        if constexpr (LUV == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
+        else k = lu_solve2(rA, rB, lane_v);
         wave_lds_sync();
         {
             const SlotState q = S.st;
@@ -704,6 +706,21 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv2(int n, const cf *__restri
     if (ok) X[(size_t)sys * NV + r] = x;
 }
 
+__global__ void __launch_bounds__(WG_THREADS) k_cgesv3(int n, const cf *__restrict__ A, const cf *__restrict__ B,
+                                                       cf *__restrict__ X) {
+    __shared__ LUBuf s_lu[2 * WAVES_PER_WG];
+    const int lane = lane_id();
+    const int r = lane & 31;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 2 + (lane >> 5);
+    const bool ok = sys < n && r < NV;
+    cf rA[NV];
+#pragma unroll
+    for (int c = 0; c < NV; c++) rA[c] = ok ? A[((size_t)sys * NV + r) * NV + c] : cmk(0.0f, 0.0f);
+    const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
+    const cf x = lu_solve3(rA, rB, lane, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)]);
+    if (ok) X[(size_t)sys * NV + r] = x;
+}
+
 __global__ void __launch_bounds__(WG_THREADS) k_eval2(int n, TableWS *ws, const cf *__restrict__ X,
                                                       const cf *__restrict__ P, const cf *__restrict__ D,
                                                       cf *__restrict__ HX, cf *__restrict__ HT, cf *__restrict__ H) {
@@ -745,23 +762,23 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval2(int n, TableWS *ws, const 
 }
 
 // ---------------------------------------------------------------- host side
-// HC_TRIFOCAL_KERNEL=v1 selects the one-path-per-wave kernels (A/B baseline);
-// default: v2 (two paths per wave).
+// HC_TRIFOCAL_KERNEL=v1|v2 selects an earlier tracker generation (A/B
+// baselines); default v3 (two paths per wave, LDS-broadcast LU).
 static int kernel_version() {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("HC_TRIFOCAL_KERNEL");
-        v = (e && e[0] == 'v' && e[1] == '1') ? 1 : 2;
+        v = (e && e[0] == 'v' && e[1] == '1') ? 1 : (e && e[0] == 'v' && e[1] == '2') ? 2 : 3;
     }
     return v;
 }
-// HC_TRIFOCAL_MINWAVES=2|3: register budget of the v2 tracker (waves per SIMD);
-// 3 (<= 168 VGPRs, measured 12 % faster than 2) is the default
-static int v2_minwaves() {
+// HC_TRIFOCAL_MINWAVES=3|4: register budget of the v3 tracker (waves per SIMD);
+// 4 (<= 128 VGPRs) measured 8 % faster than 3 on MI355X (r6) and is the default
+static int v3_minwaves() {
     static int w = -1;
     if (w < 0) {
         const char *e = getenv("HC_TRIFOCAL_MINWAVES");
-        w = (e && e[0] == '2') ? 2 : 3;
+        w = (e && e[0] == '3') ? 3 : 4;
     }
     return w;
 }
@@ -828,12 +845,13 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.stats = t->stats;
     k.ws = ws;
     k.ws2 = ws2_of(ws);
-    const bool v2 = kernel_version() == 2;
-    const bool w3 = v2_minwaves() == 3;
-    const void *kern = v2 ? (abort_mode ? (w3 ? (const void *)k_track2<true, 3> : (const void *)k_track2<true, 2>)
-                                        : (w3 ? (const void *)k_track2<false, 3> : (const void *)k_track2<false, 2>))
-                          : (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>);
-    const int grid = grid_for(v2 ? (int)((paths + 1) / 2) : (int)paths, kern);
+    const int ver = kernel_version();
+    const bool w4 = v3_minwaves() == 4;
+    const void *kern = ver == 1   ? (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>)
+                       : ver == 2 ? (abort_mode ? (const void *)k_track2<true, 3, 2> : (const void *)k_track2<false, 3, 2>)
+                       : w4       ? (abort_mode ? (const void *)k_track2<true, 4, 3> : (const void *)k_track2<false, 4, 3>)
+                                  : (abort_mode ? (const void *)k_track2<true, 3, 3> : (const void *)k_track2<false, 3, 3>);
+    const int grid = grid_for(ver >= 2 ? (int)((paths + 1) / 2) : (int)paths, kern);
     if (grid <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
         k.num_edgels = ab->num_triplet_edgels;
@@ -841,14 +859,10 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
         k.K = ab->intrinsic_matrix;
         k.found_flag = ab->found_trifocal_sols;
         k.batch_index = ab->trifocal_sols_batch_index;
-        if (v2 && w3) hipLaunchKernelGGL((k_track2<true, 3>), dim3(grid), dim3(WG_THREADS), 0, s, k);
-        else if (v2) hipLaunchKernelGGL((k_track2<true, 2>), dim3(grid), dim3(WG_THREADS), 0, s, k);
-        else hipLaunchKernelGGL(k_track<true>, dim3(grid), dim3(WG_THREADS), 0, s, k);
-    } else {
-        if (v2 && w3) hipLaunchKernelGGL((k_track2<false, 3>), dim3(grid), dim3(WG_THREADS), 0, s, k);
-        else if (v2) hipLaunchKernelGGL((k_track2<false, 2>), dim3(grid), dim3(WG_THREADS), 0, s, k);
-        else hipLaunchKernelGGL(k_track<false>, dim3(grid), dim3(WG_THREADS), 0, s, k);
     }
+    void *kargs[] = {&k};
+    g_last_hip_error = hipLaunchKernel(kern, dim3(grid), dim3(WG_THREADS), kargs, 0, s);
+    if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
     return launch_status(HC_ERROR_LAUNCH);
 }
 
@@ -881,7 +895,11 @@ hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, h
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
     (void)hipGetLastError();
-    if (hc::kernel_version() == 2) {
+    if (hc::kernel_version() == 3) {
+        const int per = 2 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_cgesv3, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+                           (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+    } else if (hc::kernel_version() == 2) {
         const int per = 2 * hc::WAVES_PER_WG;
         hipLaunchKernelGGL(hc::k_cgesv2, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
                            (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
@@ -905,7 +923,7 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
     if ((hc::g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
     hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(64), 0, s, unified_index, ws, nullptr);
     if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-    if (hc::kernel_version() == 2) {
+    if (hc::kernel_version() >= 2) {
         const int per = 2 * hc::WAVES_PER_WG;
         hipLaunchKernelGGL(hc::k_eval2, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
                            (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
@@ -921,8 +939,13 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
 const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
 
 const char *hc_trifocal_version(void) {
-    return hc::kernel_version() == 2 ? "hc_trifocal gfx950 v2 (2 paths/wave, register LU, per-lane term lists)"
-                                     : "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
+    switch (hc::kernel_version()) {
+    case 1: return "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
+    case 2: return "hc_trifocal gfx950 v2 (2 paths/wave, bpermute LU, per-lane term lists)";
+    default:
+        return hc::v3_minwaves() == 4 ? "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, 4 waves/SIMD)"
+                                      : "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, 3 waves/SIMD)";
+    }
 }
 
 }  // extern "C"

@@ -1,0 +1,203 @@
+// hc_lu3.hpp -- v3 LU of the two-paths-per-wave tracker.
+//
+// Same semantics as lu_solve() / lu_solve2() (dev-cgesv-batched-small.cuh:38-107:
+// partial pivot on |re|+|im|, first-max ties, rowid relabelling, zero pivot ->
+// recip 1, cuCdivf back substitution), restructured for the CDNA4 issue limits
+// measured on v2 (profiles/r1_v2_pmc_summary.json: VALU issue ~70 % busy, LDS
+// issue stalls 23 % of wave time):
+//
+//  * pivot-row broadcast through LDS: the pivot lane of each half writes its
+//    row (+ rhs + rowid) into a per-half buffer with ds_write_b128 and every
+//    lane reads it back with broadcast ds_read_b128 -- K/2 + K/2 LDS
+//    instructions per step instead of 2K ds_bpermute;
+//  * the cuCdivf factors of position i are parked in LDS by the pivot lane
+//    (no per-lane select bookkeeping), and since the lane with final rowid i
+//    owns position i, the back substitution needs no permutation array;
+//  * 1/s and 1/s2 use the rcp + 6-FMA core of the IEEE division sequence when
+//    s is in [2^-90, 2^120] (there v_div_scale / v_div_fixup are identities,
+//    v_div_fmas is a plain fma -- identical bits), the IEEE '/' otherwise;
+//  * cuCdivf(1, y) is evaluated as ((o1*brs)*o2, -(o1*bis)*o2), which equals
+//    the literal formula except for the sign of exact zeros.
+//
+// The buffer aliases the per-path dH/dx entry block (SlotLDS::ent), which is
+// dead between the gather of the Jacobian into registers and the next eval.
+#pragma once
+
+#include "hc_track2.hpp"
+
+namespace hc {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+struct alignas(16) LUBuf {
+    cf row[32];    // current pivot row: [0..29] A, [30] rhs, [31].x = rowid (int bits); reused for x in the back sub
+    divf f[32];    // cuCdivf factors of position i
+};
+static_assert(sizeof(divf) == 16, "divf layout");
+static_assert(sizeof(LUBuf) <= sizeof(cf) * NV * 7, "LUBuf must fit in SlotLDS::ent");
+static_assert(offsetof(SlotLDS, ent) % 16 == 0, "SlotLDS::ent must be 16-B aligned");
+
+constexpr int LU3_CHUNK = 6;   // update columns per LDS batch (even)
+
+// correctly rounded 1/s for s in [2^-90, 2^120]: the core of the IEEE f32
+// division lowering (div_scale/div_fmas/div_fixup are identities there)
+__device__ __forceinline__ float rcp_rn(float s) {
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float e0 = __builtin_fmaf(-s, r0, 1.0f);
+    const float r1 = __builtin_fmaf(e0, r0, r0);
+    const float e1 = __builtin_fmaf(-s, r1, 1.0f);
+    const float q1 = __builtin_fmaf(e1, r1, r1);
+    const float e2 = __builtin_fmaf(-s, q1, 1.0f);
+    return __builtin_fmaf(e2, r1, q1);
+}
+__device__ __forceinline__ bool rcp_fast_ok(float s) { return s >= 0x1p-90f && s <= 0x1p+120f; }
+
+__device__ __forceinline__ void st4(cf *p, cf a, cf b) {
+    f4v v = {a.x, a.y, b.x, b.y};
+    *reinterpret_cast<f4v *>(p) = v;
+}
+__device__ __forceinline__ void ld4(const cf *p, cf &a, cf &b) {
+    const f4v v = *reinterpret_cast<const f4v *>(p);
+    a = cmk(v.x, v.y);
+    b = cmk(v.z, v.w);
+}
+
+// pivot lane: row elements J.. of the register row into the buffer
+template <int J>
+__device__ __forceinline__ void lu3_put_row(const cf (&rA)[NV], LUBuf &L) {
+    if constexpr (J < NV) {
+        if constexpr (J & 1) {
+            L.row[J] = rA[J];
+            lu3_put_row<J + 1>(rA, L);
+        } else {
+            st4(&L.row[J], rA[J], rA[J + 1]);
+            lu3_put_row<J + 2>(rA, L);
+        }
+    }
+}
+
+// a_j -= l * u_j for j in [J0, NV), u from the broadcast buffer
+template <int J0>
+__device__ __forceinline__ void lu3_update(cf (&rA)[NV], const cf &l, bool below, const LUBuf &L) {
+    if constexpr (J0 < NV) {
+        if constexpr (J0 & 1) {
+            const cf u = L.row[J0];
+            if (below) rA[J0] = cmsub(rA[J0], l, u);
+            lu3_update<J0 + 1>(rA, l, below, L);
+        } else {
+            constexpr int N = (NV - J0) < LU3_CHUNK ? (NV - J0) : LU3_CHUNK;
+            cf u[N];
+#pragma unroll
+            for (int q = 0; q < N; q += 2) ld4(&L.row[J0 + q], u[q], u[q + 1]);
+            if (below) {
+#pragma unroll
+                for (int q = 0; q < N; q++) rA[J0 + q] = cmsub(rA[J0 + q], l, u[q]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            lu3_update<J0 + N>(rA, l, below, L);
+        }
+    }
+}
+
+template <int I>
+__device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, int lane, int r, int hb,
+                                            bool row_lane, LUBuf &L) {
+    if constexpr (I < NV) {
+        const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
+        const bool elig = rowid >= I && row_lane;
+        const bool isn = v != v;
+        const int key = (elig && !isn) ? __float_as_int(v) : -1;   // |.|+|.| >= +0: bits order like ints
+        const int mx = half_max_int(key);
+        const unsigned long long m = __ballot(elig && key == mx);
+        const unsigned long long nanm = __ballot(elig && isn && rowid == I);
+        const unsigned mlo = (unsigned)m & 0x3FFFFFFFu, mhi = (unsigned)(m >> 32) & 0x3FFFFFFFu;
+        int pl;   // absolute pivot lane of this lane's half
+        float piv_abs;
+        if (__builtin_expect(nanm != 0ull || __builtin_popcount(mlo) > 1 || __builtin_popcount(mhi) > 1, 0)) {
+            // rare: NaN at position I wins (:57-64); exact ties: first position wins
+            const unsigned nlo = (unsigned)nanm, nhi = (unsigned)(nanm >> 32);
+            const unsigned mine_m = hb ? mhi : mlo, mine_n = hb ? nhi : nlo;
+            const int cand = ((mine_m >> r) & 1u) ? rowid : (1 << 20);
+            const int mn = half_min_i(cand);
+            const unsigned long long w = __ballot(row_lane && rowid == mn);
+            const unsigned wm = hb ? (unsigned)(w >> 32) : (unsigned)w;
+            pl = mine_n ? hb + __builtin_ctz(mine_n) : hb + (wm ? __builtin_ctz(wm) : 0);
+            piv_abs = mine_n ? __builtin_nanf("") : __int_as_float(mx);
+        } else {
+            pl = hb ? (32 + (mhi ? __builtin_ctz(mhi) : 0)) : (mlo ? __builtin_ctz(mlo) : 0);
+            piv_abs = __int_as_float(mx);
+        }
+        const bool is_piv = lane == pl;
+        if (is_piv) {                                          // pivot row -> buffer
+            lu3_put_row<I>(rA, L);
+            L.row[30] = rB;
+            L.row[31].x = __int_as_float(rowid);
+        }
+        wave_lds_sync();                                       // cross-lane: pivot lane -> all lanes
+        const cf sxi = L.row[I];
+        cf sB0, pr;
+        ld4(&L.row[30], sB0, pr);
+        const int piv_pos = __float_as_int(pr.x);
+        if (is_piv) rowid = I;                                 // :70-82
+        else if (rowid == I) rowid = piv_pos;
+        // cuCdivf factors of the pivot (:84)
+        divf f;
+        cf reg;
+        const bool zero = (piv_abs == 0.0f);                   // :66
+        const float s = __builtin_fabsf(sxi.x) + __builtin_fabsf(sxi.y);
+        if (__builtin_expect(__ballot(!rcp_fast_ok(s)) == 0ull, 1)) {
+            f.o1 = rcp_rn(s);
+            f.brs = sxi.x * f.o1;
+            f.bis = sxi.y * f.o1;
+            const float s2 = (f.brs * f.brs) + (f.bis * f.bis);   // in [0.5, 1]
+            f.o2 = rcp_rn(s2);
+            reg = cmk((f.o1 * f.brs) * f.o2, (-(f.o1 * f.bis)) * f.o2);
+        } else {
+            f = cdiv_factors(sxi);
+            reg = cdiv_apply(cmk(1.0f, 0.0f), f);
+        }
+        if (zero) reg = cmk(1.0f, 0.0f);
+        if (is_piv) *reinterpret_cast<f4v *>(&L.f[I]) = f4v{f.o1, f.brs, f.bis, f.o2};
+        const bool below = rowid > I;                          // :86-93
+        cf l = cmk(0.0f, 0.0f);
+        if (below) {
+            l = cmul(rA[I], reg);
+            rA[I] = l;
+            rB = cmsub(rB, l, sB0);
+        }
+        lu3_update<I + 1>(rA, l, below, L);
+        lu3_forward<I + 1>(rA, rB, rowid, lane, r, hb, row_lane, L);
+    }
+}
+
+// back substitution (:97-106): the lane with rowid == I owns position I and
+// its factors; it computes x_I and publishes it in row[I]
+template <int I>
+__device__ __forceinline__ void lu3_backward(const cf (&rA)[NV], cf &rB, int rowid, const divf &myf, LUBuf &L) {
+    if constexpr (I >= 0) {
+        const cf cand = cdiv_apply(rB, myf);
+        if (rowid == I) L.row[I] = cand;
+        wave_lds_sync();
+        const cf xi = L.row[I];
+        if (rowid < I) rB = cmsub(rB, xi, rA[I]);
+        lu3_backward<I - 1>(rA, rB, rowid, myf, L);
+    }
+}
+
+// Solves the system of each half; L is this half's buffer (16-B aligned).
+__device__ __forceinline__ cf lu_solve3(cf (&rA)[NV], cf rB, int lane, LUBuf &L) {
+    const int r = lane & 31, hb = lane & 32;
+    const bool row_lane = r < NV;
+    int rowid = row_lane ? r : 99;   // padding lanes never pivot
+    lu3_forward<0>(rA, rB, rowid, lane, r, hb, row_lane, L);
+    wave_lds_sync();
+    const f4v mf = *reinterpret_cast<const f4v *>(&L.f[row_lane ? rowid : 0]);
+    divf myf;
+    myf.o1 = mf.x; myf.brs = mf.y; myf.bis = mf.z; myf.o2 = mf.w;
+    lu3_backward<NV - 1>(rA, rB, rowid, myf, L);
+    wave_lds_sync();
+    return L.row[row_lane ? r : 0];
+}
+
+}  // namespace hc

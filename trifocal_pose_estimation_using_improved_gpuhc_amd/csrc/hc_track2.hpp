@@ -43,7 +43,7 @@ struct SlotState {
     int pad;
 };
 // per path-slot LDS block
-struct SlotLDS {
+struct alignas(16) SlotLDS {
     cf x[32];        // current track (x[30] = 1)
     cf xl[32];       // last successful track
     cf sols[32];     // RK accumulator
@@ -204,6 +204,7 @@ __device__ __forceinline__ void eval_hx2(cf (&rA)[NV], const uint32_t *s_hx2, in
                                          SlotLDS &S, int r) {
     cf acc = cmk(0.0f, 0.0f);
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
+    if (r < NV) ent_row[6] = cmk(0.0f, 0.0f);   // structural zero (the v3 LU reuses this block)
     for (int k = 0; k < hx_len; k++) {
         const uint32_t w = s_hx2[k * 32 + r];
         const int co = sext4(w);
