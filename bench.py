@@ -41,9 +41,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--samples", type=int, default=100, help="RANSAC samples per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-samples", type=int, default=24, help="samples in the bounded CPU baseline run")
+    ap.add_argument("--cpu-samples", type=int, default=160,
+                    help="samples in the bounded CPU baseline run (~15 s on 16 host cores)")
     ap.add_argument("--abort-samples", type=int, default=1000,
-                    help="samples of the early-abort (config 3) time-to-first-good-pose run; 0 disables")
+                    help="samples per GPU of the early-abort (config 3/4) time-to-first-good-pose run; 0 disables")
+    ap.add_argument("--abort-chunk", type=int, default=125,
+                    help="samples per launch in the early-abort run (the cross-GPU flag is reduced between launches)")
     return ap.parse_args()
 
 
@@ -123,29 +126,53 @@ def main():
     paths = 312 * S * world
     value = paths / (ms_per_step / 1e3)
 
-    # ---- early-abort (config 3) time-to-first-good-pose, rank-local, reported only
+    # ---- early abort (config 3 at N=1, config 4 at N=8): time-to-first-good-pose.
+    # Every rank tracks its gpu-major shard of abort_samples*world samples in
+    # chunks; the found flag is max-reduced over ranks (RCCL) after each chunk
+    # (sharding.run_abort_chunks), so all ranks stop once any rank has a pose.
     abort_info = None
-    if args.abort_samples > 0 and rank == 0:
+    if args.abort_samples > 0:
+        from trifocal_pose_estimation_using_improved_gpuhc_amd import sharding
         Sa = args.abort_samples
-        ta, da, _ = prepare_target_params(problem, data, seed=0, num_samples=Sa)
-        ta = torch.from_numpy(ta).to(dev)
-        da = torch.from_numpy(da).to(dev)
+        ta_all, da_all, _ = prepare_target_params(problem, data, seed=0, num_samples=Sa * world, num_gpus=world)
+        off, cnt = sharding.shard(Sa * world, world, rank)
+        ta = torch.from_numpy(ta_all[off:off + cnt]).to(dev)
+        da = torch.from_numpy(da_all[off:off + cnt]).to(dev)
         tr.set_ransac_data(data)
-        ra = tr.allocate(Sa, stats=True, abort=True)
-        ttfp, wall = [], []
+        ra = tr.allocate(cnt, stats=True, abort=True)
+        wss = []
+        ttfp, wall, tracked = [], [], []
         for _ in range(3):
             tr.reset_tracks(ra)
             torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
             w0 = time.perf_counter()
-            tr.launch(ta, da, ra, abort=True, stream=stream)
+            tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream)
             torch.cuda.synchronize(dev)
-            wall.append(time.perf_counter() - w0)
-            ttfp.append(tr.first_found_seconds())
-        ha = ra.host()
-        abort_info = {"samples": Sa, "found": bool(ha["found"]),
-                      "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3),
+            w = time.perf_counter() - w0
+            hz = tr.read_timestamps(wss[0])[2]
+            f = sharding.first_found_seconds([tr.read_timestamps(x)[:2] for x in wss[:len(sharding.chunks(cnt, args.abort_chunk))]], hz)
+            n_tr = int((ra.stats[:, 0] > 0).sum().item())
+            if world > 1:
+                v = torch.tensor([f if f >= 0 else 1e30, -w, -float(n_tr)], dtype=torch.float64, device=dev)
+                dist.all_reduce(v, op=dist.ReduceOp.MIN)
+                f, w = float(v[0].item()), -float(v[1].item())
+                f = -1.0 if f >= 1e29 else f
+                nt = torch.tensor([n_tr], dtype=torch.int64, device=dev)
+                dist.all_reduce(nt)
+                n_tr = int(nt.item())
+            ttfp.append(f)
+            wall.append(w)
+            tracked.append(n_tr)
+        found = bool(ra.found.item())
+        abort_info = {"samples_total": Sa * world, "samples_per_gpu": Sa, "chunk_samples": args.abort_chunk,
+                      "found": found,
+                      "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3) if found else None,
                       "kernel_exit_wall_ms": round(float(np.median(wall)) * 1e3, 3),
-                      "paths_tracked": int((ha["stats"]["steps"] > 0).sum())}
+                      "paths_tracked": int(np.median(tracked)),
+                      "note": "device clock (s_memrealtime) from the first chunk's start, min over ranks; "
+                              "wall = host time to the all-GPU sync, max over ranks"}
 
     if rank == 0:
         med_launch_s = float(np.median(launch_ms)) / 1e3
@@ -171,7 +198,11 @@ def main():
                        "GPUHC_Max_Correction_Steps": tr.settings.max_corrections,
                        "kernel": _abi.lib().hc_trifocal_version().decode()},
             "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4), "traffic": None,
+                         "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
+                         "traffic": traffic_bytes(_abi.lib().hc_trifocal_version().decode()),
+                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 gfx950 correction + "
+                                         "WRITE_SIZE, committed profiles/*_pmc_summary.json of this kernel "
+                                         "version; algorithmic ~0.5 KB/path = 15.3 MB/launch)",
                          "note": "FP32-compute (VALU) bound tracker kernel; MI355X FP32 vector peak == FP32 MFMA "
                                  "peak (157.3 TF). achieved = algorithmic FLOPs of the executed stages "
                                  "(SURVEY 8d: 104.3 kFLOP/predictor stage, 101.3 kFLOP/corrector stage) / median "
@@ -188,6 +219,22 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def traffic_bytes(version):
+    """HBM bytes per tracker launch from the newest committed PMC summary of
+    this kernel version (PMC counters cannot be collected inside the timed run)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        if d.get("version") == version and "hbm_bytes_per_launch" in d.get("derived", {}):
+            best = d["derived"]["hbm_bytes_per_launch"]
+    return best
 
 
 def cpu_baseline(problem, data, n_samples, gpu_value):

@@ -124,6 +124,14 @@ hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAb
    Reads the workspace with a blocking copy -- call after synchronising. */
 hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_seconds);
 
+/* Raw device clock of the last launch on this workspace (s_memrealtime, a
+   constant-rate counter shared by every launch on the device; *tick_hz = its
+   rate): start = first workgroup of the tracker began, found = first good
+   hypothesis (0 if none).  Lets a caller that splits its samples into several
+   launches (one workspace each) measure time-to-first-good-pose across them. */
+hcStatus hc_trifocal_read_timestamps(const void *workspace, uint64_t *start_ticks, uint64_t *found_ticks,
+                                     double *tick_hz);
+
 /* ---- component entry points (batched building blocks, also used by tests) ---- */
 
 /* Batched 30x30 complex solve with the tracker's LU (partial pivoting on

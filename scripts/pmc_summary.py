@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh run: per-launch PMC counters of the tracker
+kernel plus derived utilisations.  usage: pmc_summary.py TAG [out.json] [kernel version string]"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+tag = sys.argv[1]
+base = os.path.join(ROOT, "gpurun_out")
+KPFX = "void hc::k_track"
+stats = list(csv.DictReader(open(os.path.join(base, f"{tag}_trace", "run_kernel_stats.csv"))))
+trk = [r for r in stats if r["Name"].startswith(KPFX)][0]
+out = {"tag": tag, "version": sys.argv[3] if len(sys.argv) > 3 else None, "kernel": trk["Name"], "calls": int(trk["Calls"]), "avg_ns": float(trk["AverageNs"]),
+       "min_ns": float(trk["MinNs"]), "max_ns": float(trk["MaxNs"]), "counters": {}}
+meta = None
+for d in sorted(glob.glob(os.path.join(base, f"{tag}_pmc*"))):
+    f = os.path.join(d, "run_counter_collection.csv")
+    if not os.path.exists(f):
+        continue
+    agg = collections.defaultdict(float)
+    disp = set()
+    for r in csv.DictReader(open(f)):
+        if r["Kernel_Name"].startswith(KPFX):
+            agg[r["Counter_Name"]] += float(r["Counter_Value"])
+            disp.add(r["Dispatch_Id"])
+            meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",
+                                      "Accum_VGPR_Count", "SGPR_Count")}
+    for k, v in agg.items():
+        out["counters"][k] = v / max(1, len(disp))
+out["dispatch"] = meta
+c = out["counters"]
+der = {}
+if "SQ_WAVES" in c:
+    waves = c["SQ_WAVES"]
+    cyc = c["SQ_WAVE_CYCLES"] * 4 / waves              # quad-cycles -> cycles per wave
+    der["waves"] = waves
+    der["cycles_per_wave"] = cyc
+    der["eff_clock_ghz"] = cyc / out["avg_ns"]
+    simds = 256 * 4
+    der["valu_issue_busy"] = c["SQ_INSTS_VALU"] / simds * 4 / cyc      # wave64 VALU = 4 cycles/instr
+    der["valu_per_wave"] = c["SQ_INSTS_VALU"] / waves
+    der["lds_per_wave"] = c["SQ_INSTS_LDS"] / waves
+    der["frac_wait_inst_any"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    der["frac_wait_any"] = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    if "SQ_ACTIVE_INST_ANY" in c:
+        der["frac_active_any"] = c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+        der["frac_wait_inst_lds"] = c["SQ_WAIT_INST_LDS"] / c["SQ_WAVE_CYCLES"]
+        der["salu_per_wave"] = c["SQ_INSTS_SALU"] / waves
+    if "SQC_ICACHE_MISSES" in c:
+        der["icache_miss_rate"] = c["SQC_ICACHE_MISSES"] / max(1.0, c["SQC_ICACHE_MISSES"] + c["SQC_ICACHE_HITS"])
+if "FETCH_SIZE" in c:
+    der["hbm_fetch_bytes_corrected"] = c["FETCH_SIZE"] * 1024 * 2      # MI355X_MICROARCH.md: x2 on gfx950
+if "WRITE_SIZE" in c:
+    der["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
+if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+    der["hbm_bytes_per_launch"] = der["hbm_fetch_bytes_corrected"] + der["hbm_write_bytes"]
+out["derived"] = der
+s = json.dumps(out, indent=1)
+print(s)
+if len(sys.argv) > 2:
+    open(sys.argv[2], "w").write(s + "\n")

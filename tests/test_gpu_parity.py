@@ -154,3 +154,44 @@ def test_tracker_abort_mode(problem, samples100, tracker):
         if st["inliers21"][b] or st["inliers31"][b] or ok:
             assert (st["inliers21"][b], st["inliers31"][b]) == (i21, i31)
     assert tracker.first_found_seconds() > 0
+
+
+@pytest.mark.gpu
+def test_tracker_abort_chunked(problem, samples100, tracker):
+    """The multi-GPU early-stop protocol on one rank: 100 samples in chunks of
+    10 launches, one workspace each.  Found ids (made global) are passing
+    hypotheses, tracked paths equal the abort-off golden run, and once a chunk
+    has found a pose every later chunk skips all of its paths."""
+    import sys
+
+    import torch
+
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import sharding
+    sys.path.insert(0, GOLDEN)
+    from make_golden import track_hash
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    passing = set(int(b) for b, s in zip(g["scored_ids"], g["scored"]) if s[0] == 1)
+    tgt, dif, _ = samples100
+    dev = tracker.device
+    t = torch.from_numpy(tgt).to(dev)
+    d = torch.from_numpy(dif).to(dev)
+    r = tracker.allocate(100, stats=True, abort=True)
+    tracker.reset_tracks(r)
+    wss = []
+    parts = tracker.launch_abort_chunked(t, d, r, chunk_samples=10, workspaces=wss)
+    torch.cuda.synchronize(dev)
+    h = r.host()
+    assert len(parts) == 10 and h["found"]
+    found = set()
+    for off, n in parts:
+        loc = h["batch_index"][off * 312:(off + n) * 312]
+        found |= set(int(b) for b in sharding.global_batch_ids(loc, off, 0))
+    assert found and found <= passing
+    tracked = h["stats"]["steps"] > 0
+    assert (h["converge"][tracked] == g["conv"][tracked]).all()
+    assert (track_hash(h["tracks"])[tracked] == g["hash"][tracked]).all()
+    first_chunk = min(b // 312 for b in found) // 10
+    assert not tracked[(first_chunk + 1) * 3120:].any()
+    stamps = [tracker.read_timestamps(w)[:2] for w in wss]
+    hz = tracker.read_timestamps(wss[0])[2]
+    assert sharding.first_found_seconds(stamps, hz) > 0

@@ -46,6 +46,7 @@ struct KArgs {
     hcPathStats *stats;
     TableWS *ws;
     TableWS2 *ws2;
+    TableWS3 *ws3;
     // abort mode
     int num_edgels;
     const float *edgels;
@@ -163,10 +164,78 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
         const int len = min(w2->hx_len, HX2_SLOT_CAP);
         for (int k2 = s_len[r]; k2 < len; k2++) w2->hx[k2 * 32 + r] = 0u;
     }
+    // ---- v3: the same per-lane term lists as LDS byte offsets (hc_eval3.hpp)
+    TableWS3 *w3 = (TableWS3 *)((char *)w2 + ((sizeof(TableWS2) + 255) & ~(size_t)255));
+    __shared__ int s_bad;
+    if (r == 0) s_bad = 0;
+    __syncthreads();
+    const uint2 pad_hx = make_uint2((uint32_t)(SLOT_OFF_P + 8 * 33) | ((uint32_t)(SLOT_OFF_P + 8 * 33) << 16),
+                                    (uint32_t)(SLOT_OFF_X + 8 * 30) | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 8));
+    if (r < 32) {
+        int n = 0, slot = 0;
+        bool bad = false;
+        if (r < NV) {
+            for (int c = 0; c < NV; c++) {
+                int last_j = -1;
+                for (int j = 0; j < HX_TERMS; j++)
+                    if (U[(c * HX_TERMS + j) * HX_PARTS * NV + r] != 0) last_j = j;
+                if (last_j < 0) continue;
+                for (int j = 0; j <= last_j; j++) {
+                    const int base = (c * HX_TERMS + j) * HX_PARTS * NV + r;
+                    const int co = U[base], a = U[base + NV], b = U[base + 2 * NV], u = U[base + 3 * NV],
+                              v = U[base + 4 * NV];
+                    if (co == 0) continue;
+                    bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
+                           v < 0 || v > NV || slot >= 6;
+                    if (n < HX3_SLOT_CAP && !bad)
+                        w3->hx[n * 32 + r] = make_uint2(
+                            (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
+                            (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
+                                (((uint32_t)co & 0xFFu) << 16) | ((uint32_t)(8 * slot) << 24) |
+                                ((uint32_t)(j == last_j) << 31));
+                    n++;
+                }
+                slot++;
+            }
+        }
+        if (n > HX3_SLOT_CAP) bad = true;
+        for (int k2 = n; k2 < HX3_SLOT_CAP; k2++) w3->hx[k2 * 32 + r] = pad_hx;
+        s_len[r] = n;
+        const int32_t *D = U + HX_SIZE;
+        int k = 0;
+        if (r < NV) {
+            for (int j = 0; j < HT_TERMS; j++) {
+                const int base = j * HT_PARTS * NV + r;
+                const int co = D[base], a = D[base + NV], b = D[base + 2 * NV], u = D[base + 3 * NV],
+                          v = D[base + 4 * NV], x3 = D[base + 5 * NV];
+                if (co == 0) continue;
+                bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
+                       v < 0 || v > NV || x3 < 0 || x3 > NV;
+                if (!bad)
+                    w3->ht[k * 32 + r] = make_uint2(
+                        (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
+                        (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
+                            ((uint32_t)(SLOT_OFF_X + 8 * x3) << 16) | (((uint32_t)co & 0xFFu) << 24));
+                k++;
+            }
+        }
+        for (; k < HT_TERMS; k++) w3->ht[k * 32 + r] = make_uint2(pad_hx.x, pad_hx.y | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 16));
+        if (bad) atomicOr(&s_bad, 1);
+    }
+    __syncthreads();
+    if (r == 0) {
+        int mx = 0;
+        for (int q = 0; q < 32; q++) mx = max(mx, s_len[q]);
+        w3->hx_len = mx;
+        w3->status = s_bad ? HC_ERROR_TABLE : 0;
+    }
 }
 
 __host__ __device__ __forceinline__ TableWS2 *ws2_of(TableWS *ws) {
     return (TableWS2 *)((char *)ws + ((sizeof(TableWS) + 255) & ~(size_t)255));
+}
+__host__ __device__ __forceinline__ TableWS3 *ws3_of(TableWS *ws) {
+    return (TableWS3 *)((char *)ws2_of(ws) + ((sizeof(TableWS2) + 255) & ~(size_t)255));
 }
 
 // per-workgroup LDS
@@ -373,18 +442,30 @@ __device__ __forceinline__ int half_sum_i(int v) {
     return v;
 }
 
-template <bool ABORT, int MINW, int LUV>
+template <bool ABORT, int MINW, int V>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
-    __shared__ uint32_t s_hx2[HX2_SLOT_CAP * 32];
-    __shared__ uint32_t s_ht[HT_TERMS * 32];
+    // V = 2: bpermute LU + v2 evals; V = 3: LDS-broadcast LU + packed v3 evals
+    constexpr int TAB_BYTES = V == 3 ? (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32)
+                                     : (int)(sizeof(uint32_t) * (HX2_SLOT_CAP + HT_TERMS) * 32);
+    __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
     __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
     TableWS *ws = a.ws;
     TableWS2 *w2 = a.ws2;
-    if ((ws->status | (unsigned)w2->status) != 0u) return;
-    const int hx_len = w2->hx_len;
-    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx2[i] = w2->hx[i];
-    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht[i] = ws->ht[i];
+    TableWS3 *w3 = a.ws3;
+    if ((ws->status | (unsigned)w2->status | (V == 3 ? (unsigned)w3->status : 0u)) != 0u) return;
+    const int hx_len = V == 3 ? w3->hx_len : w2->hx_len;
+    uint32_t *s_hx2 = reinterpret_cast<uint32_t *>(s_tab);
+    uint32_t *s_ht = s_hx2 + HX2_SLOT_CAP * 32;
+    uint2 *s_hx3 = reinterpret_cast<uint2 *>(s_tab);
+    uint2 *s_ht3 = s_hx3 + HX3_SLOT_CAP * 32;
+    if constexpr (V == 3) {
+        for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];
+        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = w3->ht[i];
+    } else {
+        for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx2[i] = w2->hx[i];
+        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht[i] = ws->ht[i];
+    }
     if (threadIdx.x < NPP) s_sp[threadIdx.x] = a.start_params[threadIdx.x];
     {
         float *z = reinterpret_cast<float *>(s_slot);
@@ -573,19 +654,20 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
         const bool act = ph_in == PH_STAGE;
         const bool pred = act && s_in < 4;
         cf rA[NV];
-        eval_hx2(rA, s_hx2, hx_len, map, S, r_v);                            // :184 / :220
+        if constexpr (V == 3) eval_hx3(rA, s_hx3, hx_len, map, S, r_v);     // :184 / :220
+        else eval_hx2(rA, s_hx2, hx_len, map, S, r_v);
         cf rB = cmk(0.0f, 0.0f);
         if (__ballot(pred) != 0ull) {                                        // :185
-            const cf t = eval_ht2(s_ht, S, r_v);
+            const cf t = V == 3 ? eval_ht3(s_ht3, S, r_v) : eval_ht2(s_ht, S, r_v);
             if (pred) rB = t;
         }
         if (__ballot(act && !pred) != 0ull) {                                // :221
-            const cf t = eval_h2(s_ht, S, r_v);
+            const cf t = V == 3 ? eval_h3(s_ht3, S, r_v) : eval_h2(s_ht, S, r_v);
             if (!pred) rB = t;
         }
         wave_lds_sync();
         cf k;                                                                // :188 / :224
-        if constexpr (LUV == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
+        if constexpr (V == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
         else k = lu_solve2(rA, rB, lane_v);
         wave_lds_sync();
         {
@@ -761,6 +843,48 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval2(int n, TableWS *ws, const 
     }
 }
 
+__global__ void __launch_bounds__(WG_THREADS) k_eval3(int n, TableWS *ws, const cf *__restrict__ X,
+                                                      const cf *__restrict__ P, const cf *__restrict__ D,
+                                                      cf *__restrict__ HX, cf *__restrict__ HT, cf *__restrict__ H) {
+    __shared__ uint2 s_hx3[HX3_SLOT_CAP * 32];
+    __shared__ uint2 s_ht3[HT_TERMS * 32];
+    __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
+    const TableWS2 *w2 = ws2_of(ws);
+    const TableWS3 *w3 = ws3_of(ws);
+    if (w3->status != 0) return;
+    const int hx_len = w3->hx_len;
+    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];
+    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = w3->ht[i];
+    {
+        float *z = reinterpret_cast<float *>(s_slot);
+        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
+    }
+    __syncthreads();
+    const int lane = lane_id();
+    const int r = lane & 31;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 2 + (lane >> 5);
+    SlotLDS &S = s_slot[(threadIdx.x / WAVE) * 2 + (lane >> 5)];
+    const bool ok = sys < n;
+    if (ok && r < 31) S.x[r] = X[(size_t)sys * 31 + r];
+    if (ok) {
+        S.p[r] = P[(size_t)sys * NPP + r];
+        S.dif[r] = D[(size_t)sys * NPP + r];
+        if (r < NPP - 32) { S.p[r + 32] = P[(size_t)sys * NPP + r + 32]; S.dif[r + 32] = D[(size_t)sys * NPP + r + 32]; }
+    }
+    const uint32_t map[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
+    wave_lds_sync();
+    cf rA[NV];
+    eval_hx3(rA, s_hx3, hx_len, map, S, r);
+    const cf ht = eval_ht3(s_ht3, S, r);
+    const cf h = eval_h3(s_ht3, S, r);
+    if (ok && r < NV) {
+#pragma unroll
+        for (int c = 0; c < NV; c++) HX[((size_t)sys * NV + r) * NV + c] = rA[c];
+        HT[(size_t)sys * NV + r] = ht;
+        H[(size_t)sys * NV + r] = h;
+    }
+}
+
 // ---------------------------------------------------------------- host side
 // HC_TRIFOCAL_KERNEL=v1|v2 selects an earlier tracker generation (A/B
 // baselines); default v3 (two paths per wave, LDS-broadcast LU).
@@ -783,7 +907,8 @@ static int v3_minwaves() {
     return w;
 }
 static size_t ws_bytes_needed() {
-    return ((sizeof(TableWS) + 255) & ~(size_t)255) + ((sizeof(TableWS2) + 255) & ~(size_t)255);
+    return ((sizeof(TableWS) + 255) & ~(size_t)255) + ((sizeof(TableWS2) + 255) & ~(size_t)255) +
+           ((sizeof(TableWS3) + 255) & ~(size_t)255);
 }
 
 static int grid_for(int waves_needed, const void *kernel) {
@@ -845,6 +970,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.stats = t->stats;
     k.ws = ws;
     k.ws2 = ws2_of(ws);
+    k.ws3 = ws3_of(ws);
     const int ver = kernel_version();
     const bool w4 = v3_minwaves() == 4;
     const void *kern = ver == 1   ? (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>)
@@ -891,6 +1017,17 @@ hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_sec
     return HC_SUCCESS;
 }
 
+hcStatus hc_trifocal_read_timestamps(const void *workspace, uint64_t *start_ticks, uint64_t *found_ticks,
+                                     double *tick_hz) {
+    if (!workspace || !start_ticks || !found_ticks || !tick_hz) return HC_ERROR_INVALID_VALUE;
+    hc::TableWS h;
+    if (hipMemcpy(&h, workspace, 64, hipMemcpyDeviceToHost) != hipSuccess) return HC_ERROR_DEVICE;
+    *start_ticks = h.t_start;
+    *found_ticks = h.t_found;
+    *tick_hz = 100.0e6;   // s_memrealtime: constant 100 MHz on gfx9
+    return HC_SUCCESS;
+}
+
 hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, hcComplex *x, hcStream stream) {
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
@@ -923,7 +1060,12 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
     if ((hc::g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
     hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(64), 0, s, unified_index, ws, nullptr);
     if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-    if (hc::kernel_version() >= 2) {
+    if (hc::kernel_version() == 3) {
+        const int per = 2 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_eval3, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
+                           (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
+                           (hc::cf *)H);
+    } else if (hc::kernel_version() == 2) {
         const int per = 2 * hc::WAVES_PER_WG;
         hipLaunchKernelGGL(hc::k_eval2, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
                            (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
@@ -943,8 +1085,8 @@ const char *hc_trifocal_version(void) {
     case 1: return "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
     case 2: return "hc_trifocal gfx950 v2 (2 paths/wave, bpermute LU, per-lane term lists)";
     default:
-        return hc::v3_minwaves() == 4 ? "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, 4 waves/SIMD)"
-                                      : "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, 3 waves/SIMD)";
+        return hc::v3_minwaves() == 4 ? "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, packed evals, 4 waves/SIMD)"
+                                      : "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, packed evals, 3 waves/SIMD)";
     }
 }
 

@@ -13,9 +13,8 @@
 //  * the cuCdivf factors of position i are parked in LDS by the pivot lane
 //    (no per-lane select bookkeeping), and since the lane with final rowid i
 //    owns position i, the back substitution needs no permutation array;
-//  * 1/s and 1/s2 use the rcp + 6-FMA core of the IEEE division sequence when
-//    s is in [2^-90, 2^120] (there v_div_scale / v_div_fixup are identities,
-//    v_div_fmas is a plain fma -- identical bits), the IEEE '/' otherwise;
+//  * 1/s and 1/s2 use v_rcp_f32 + one Newton step when s is in [2^-90, 2^120)
+//    (exhaustively verified correctly rounded there), the IEEE '/' otherwise;
 //  * cuCdivf(1, y) is evaluated as ((o1*brs)*o2, -(o1*bis)*o2), which equals
 //    the literal formula except for the sign of exact zeros.
 //
@@ -23,7 +22,7 @@
 // dead between the gather of the Jacobian into registers and the next eval.
 #pragma once
 
-#include "hc_track2.hpp"
+#include "hc_eval3.hpp"
 
 namespace hc {
 
@@ -40,18 +39,16 @@ static_assert(offsetof(SlotLDS, ent) % 16 == 0, "SlotLDS::ent must be 16-B align
 
 constexpr int LU3_CHUNK = 6;   // update columns per LDS batch (even)
 
-// correctly rounded 1/s for s in [2^-90, 2^120]: the core of the IEEE f32
-// division lowering (div_scale/div_fmas/div_fixup are identities there)
+// Correctly rounded 1/s for s in [2^-90, 2^120): v_rcp_f32 plus one Newton
+// step.  Verified bit-identical to the IEEE division (hipcc's div_scale /
+// div_fmas / div_fixup sequence) for every float in that range -- all 2^23
+// significands x 210 binades, scripts/rcp_check.hip, profiles/r1_rcp_check.json.
 __device__ __forceinline__ float rcp_rn(float s) {
     const float r0 = __builtin_amdgcn_rcpf(s);
     const float e0 = __builtin_fmaf(-s, r0, 1.0f);
-    const float r1 = __builtin_fmaf(e0, r0, r0);
-    const float e1 = __builtin_fmaf(-s, r1, 1.0f);
-    const float q1 = __builtin_fmaf(e1, r1, r1);
-    const float e2 = __builtin_fmaf(-s, q1, 1.0f);
-    return __builtin_fmaf(e2, r1, q1);
+    return __builtin_fmaf(e0, r0, r0);
 }
-__device__ __forceinline__ bool rcp_fast_ok(float s) { return s >= 0x1p-90f && s <= 0x1p+120f; }
+__device__ __forceinline__ bool rcp_fast_ok(float s) { return s >= 0x1p-90f && s < 0x1p+120f; }
 
 __device__ __forceinline__ void st4(cf *p, cf a, cf b) {
     f4v v = {a.x, a.y, b.x, b.y};
@@ -109,26 +106,30 @@ __device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, in
         const bool isn = v != v;
         const int key = (elig && !isn) ? __float_as_int(v) : -1;   // |.|+|.| >= +0: bits order like ints
         const int mx = half_max_int(key);
-        const unsigned long long m = __ballot(elig && key == mx);
-        const unsigned long long nanm = __ballot(elig && isn && rowid == I);
-        const unsigned mlo = (unsigned)m & 0x3FFFFFFFu, mhi = (unsigned)(m >> 32) & 0x3FFFFFFFu;
-        int pl;   // absolute pivot lane of this lane's half
+        // key == mx alone marks the candidates: mx >= 0 unless every eligible entry is
+        // NaN, and then position I is NaN too (rare path).  Single compares ballot
+        // straight into SGPRs (an && chain would be materialised first).
+        const bool cand = key == mx;
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(cand);
+        const unsigned long long nanm = __builtin_amdgcn_ballot_w64(isn) & __builtin_amdgcn_ballot_w64(rowid == I);
+        const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
+        bool is_piv;      // this lane holds the pivot row of its half
         float piv_abs;
         if (__builtin_expect(nanm != 0ull || __builtin_popcount(mlo) > 1 || __builtin_popcount(mhi) > 1, 0)) {
             // rare: NaN at position I wins (:57-64); exact ties: first position wins
             const unsigned nlo = (unsigned)nanm, nhi = (unsigned)(nanm >> 32);
             const unsigned mine_m = hb ? mhi : mlo, mine_n = hb ? nhi : nlo;
-            const int cand = ((mine_m >> r) & 1u) ? rowid : (1 << 20);
-            const int mn = half_min_i(cand);
-            const unsigned long long w = __ballot(row_lane && rowid == mn);
+            const int c2 = ((mine_m >> r) & 1u) ? rowid : (1 << 20);
+            const int mn = half_min_i(c2);
+            const unsigned long long w = __builtin_amdgcn_ballot_w64(row_lane && rowid == mn);
             const unsigned wm = hb ? (unsigned)(w >> 32) : (unsigned)w;
-            pl = mine_n ? hb + __builtin_ctz(mine_n) : hb + (wm ? __builtin_ctz(wm) : 0);
+            const int pl = mine_n ? hb + __builtin_ctz(mine_n) : hb + (wm ? __builtin_ctz(wm) : 0);
+            is_piv = lane == pl;
             piv_abs = mine_n ? __builtin_nanf("") : __int_as_float(mx);
         } else {
-            pl = hb ? (32 + (mhi ? __builtin_ctz(mhi) : 0)) : (mlo ? __builtin_ctz(mlo) : 0);
+            is_piv = cand;   // exactly one candidate per half
             piv_abs = __int_as_float(mx);
         }
-        const bool is_piv = lane == pl;
         if (is_piv) {                                          // pivot row -> buffer
             lu3_put_row<I>(rA, L);
             L.row[30] = rB;
@@ -144,9 +145,9 @@ __device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, in
         // cuCdivf factors of the pivot (:84)
         divf f;
         cf reg;
-        const bool zero = (piv_abs == 0.0f);                   // :66
-        const float s = __builtin_fabsf(sxi.x) + __builtin_fabsf(sxi.y);
-        if (__builtin_expect(__ballot(!rcp_fast_ok(s)) == 0ull, 1)) {
+        const float s = __builtin_fabsf(sxi.x) + __builtin_fabsf(sxi.y);   // == piv_abs
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(!rcp_fast_ok(s)) == 0ull, 1)) {
+            // s in [2^-90, 2^120): non-zero, finite pivot
             f.o1 = rcp_rn(s);
             f.brs = sxi.x * f.o1;
             f.bis = sxi.y * f.o1;
@@ -155,16 +156,17 @@ __device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, in
             reg = cmk((f.o1 * f.brs) * f.o2, (-(f.o1 * f.bis)) * f.o2);
         } else {
             f = cdiv_factors(sxi);
-            reg = cdiv_apply(cmk(1.0f, 0.0f), f);
+            reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
         }
-        if (zero) reg = cmk(1.0f, 0.0f);
         if (is_piv) *reinterpret_cast<f4v *>(&L.f[I]) = f4v{f.o1, f.brs, f.bis, f.o2};
         const bool below = rowid > I;                          // :86-93
         cf l = cmk(0.0f, 0.0f);
         if (below) {
-            l = cmul(rA[I], reg);
+            const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+            const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
+            l = cmk(lp.x, lp.y);
             rA[I] = l;
-            rB = cmsub(rB, l, sB0);
+            rB = cmk(bp.x, bp.y);
         }
         lu3_update<I + 1>(rA, l, below, L);
         lu3_forward<I + 1>(rA, rB, rowid, lane, r, hb, row_lane, L);

@@ -1,0 +1,82 @@
+"""Multi-GPU sharding of RANSAC samples and the early-stop ("good pose found") flag.
+
+One process per GPU (torch.distributed; backend "nccl" == RCCL on ROCm).  RANSAC
+samples are independent, so each rank tracks its own contiguous gpu-major shard
+-- the reference's split (magmaHC/GPU_HC_Solver.cpp:85-88, 263-265) -- and the
+data path needs no collective.  RCCL carries only:
+
+  * the early-stop flag in abort mode: a rank's samples run in chunks; after
+    every chunk launch a 1-byte all_reduce(MAX) of the rank's found flag is
+    enqueued on the same stream, and the next chunk's table-prep kernel copies
+    the reduced flag into the workspace, so every rank skips its remaining
+    paths once any rank has found a passing hypothesis.  Nothing synchronises
+    with the host between chunks (stream order does it);
+  * timing (barrier, max / min over ranks) in bench.py.
+
+The reference has no cross-GPU early stop: each GPU keeps its own flag
+(GPU_HC_Solver.cpp:308-333).  With one rank the protocol reduces to the
+reference behaviour.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Tuple
+
+import numpy as np
+
+
+def shard(num_samples: int, world: int, rank: int) -> Tuple[int, int]:
+    """(offset, count) of rank's samples: N/G + (g < N%G) each, gpu-major."""
+    if world <= 0 or not 0 <= rank < world or num_samples < 0:
+        raise ValueError("bad shard request")
+    base, extra = divmod(num_samples, world)
+    count = base + (1 if rank < extra else 0)
+    offset = rank * base + min(rank, extra)
+    return offset, count
+
+
+def chunks(count: int, chunk_samples: int) -> List[Tuple[int, int]]:
+    """Split a rank's `count` samples into launches of at most chunk_samples."""
+    if chunk_samples <= 0:
+        raise ValueError("chunk_samples must be positive")
+    return [(o, min(chunk_samples, count - o)) for o in range(0, count, chunk_samples)]
+
+
+def run_abort_chunks(launch_chunk: Callable[[int, int, int], None], flag, count: int, chunk_samples: int,
+                     group=None) -> int:
+    """Early-stop protocol over this rank's samples.
+
+    launch_chunk(k, offset, n) enqueues chunk k (samples [offset, offset+n) of
+    the shard); the launch reads `flag` when it starts and sets it when a
+    passing hypothesis is found.  After each launch the flag is max-reduced
+    over all ranks (stream-ordered for RCCL; synchronous for gloo).  Returns
+    the number of chunks enqueued (always all of them: a chunk that starts
+    with the flag set skips its paths on the device, so no host round trip is
+    needed to stop).
+    """
+    import torch.distributed as dist
+    parts = chunks(count, chunk_samples)
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    for k, (off, n) in enumerate(parts):
+        launch_chunk(k, off, n)
+        if multi:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    return len(parts)
+
+
+def first_found_seconds(stamps: List[Tuple[int, int]], tick_hz: float) -> float:
+    """Time from the first chunk's start to the earliest found stamp of this
+    rank's chunk workspaces ((start_ticks, found_ticks) per chunk, 0 = none);
+    -1 if nothing was found."""
+    starts = [s for s, _ in stamps if s]
+    found = [f for _, f in stamps if f]
+    if not starts or not found:
+        return -1.0
+    return float(min(found) - min(starts)) / tick_hz
+
+
+def global_batch_ids(local_batch_index: np.ndarray, chunk_offset: int, shard_offset: int) -> np.ndarray:
+    """Batch ids written by a chunk launch (b = sample*312 + track within the
+    launch, reference layout) -> ids in the whole RANSAC run."""
+    ids = np.asarray(local_batch_index)
+    ids = ids[ids >= 0]
+    return ids + 312 * (chunk_offset + shard_offset)

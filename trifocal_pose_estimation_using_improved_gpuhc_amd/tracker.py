@@ -100,26 +100,39 @@ class DeviceTracker:
             r.batch_index.fill_(-1)
 
     def launch(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, abort: bool = False,
-               stream: torch.cuda.Stream | None = None) -> None:
-        """Enqueue one tracking run on `stream` (no synchronisation)."""
-        num_samples = target.shape[0]
+               stream: torch.cuda.Stream | None = None, workspace: torch.Tensor | None = None,
+               sample_offset: int = 0, num_samples: int | None = None) -> None:
+        """Enqueue one tracking run on `stream` (no synchronisation).
+
+        Samples [sample_offset, sample_offset + num_samples) of `target`/`diff`
+        are tracked into the matching rows of `r` (defaults: all of them); the
+        launch's batch ids (abort-mode batch_index values) are local to it."""
+        if num_samples is None:
+            num_samples = target.shape[0] - sample_offset
+        if num_samples < 0 or sample_offset < 0 or sample_offset + num_samples > target.shape[0] or \
+                (sample_offset + num_samples) * 312 > r.tracks.shape[0]:
+            raise _abi.HCError("sample range outside the buffers")
+        p0, p1 = sample_offset * 312, (sample_offset + num_samples) * 312
+        ws_t = workspace if workspace is not None else self.workspace
+        if ws_t.numel() < self.ws_bytes:
+            raise _abi.HCError("workspace too small")
         a = _abi.hcTrackArgs()
         a.sub_ransac_iters = num_samples
         a.settings = self.settings
         a.start_sols = self.start_sols.data_ptr()
         a.start_sols_array = None
-        a.tracks = r.tracks.data_ptr()
+        a.tracks = r.tracks[p0:p1].data_ptr()
         a.track_array = None
         a.start_params = self.start_params.data_ptr()
-        a.target_params = target.data_ptr()
-        a.diff_params = diff.data_ptr()
+        a.target_params = target[sample_offset:].data_ptr()
+        a.diff_params = diff[sample_offset:].data_ptr()
         a.unified_index = self.unified.data_ptr()
-        a.converge = r.converge.data_ptr()
-        a.infinity = r.infinity.data_ptr()
-        a.stats = r.stats.data_ptr() if r.stats is not None else None
+        a.converge = r.converge[p0:p1].data_ptr()
+        a.infinity = r.infinity[p0:p1].data_ptr()
+        a.stats = r.stats[p0:p1].data_ptr() if r.stats is not None else None
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         hs = C.c_void_p(s.cuda_stream)
-        ws = C.c_void_p(self.workspace.data_ptr())
+        ws = C.c_void_p(ws_t.data_ptr())
         if abort:
             if self.edgels is None:
                 raise _abi.HCError("abort mode needs set_ransac_data() first")
@@ -128,12 +141,39 @@ class DeviceTracker:
             ab.triplet_edge_locations = self.edgels.data_ptr()
             ab.intrinsic_matrix = self.K.data_ptr()
             ab.found_trifocal_sols = r.found.data_ptr()
-            ab.trifocal_sols_batch_index = r.batch_index.data_ptr()
+            ab.trifocal_sols_batch_index = r.batch_index[p0:p1].data_ptr()
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track_abort")
         else:
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track(C.byref(a), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track")
+
+    def new_workspace(self) -> torch.Tensor:
+        return torch.zeros(self.ws_bytes, dtype=torch.uint8, device=self.device)
+
+    def launch_abort_chunked(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, chunk_samples: int,
+                             workspaces: list, group=None, stream: torch.cuda.Stream | None = None) -> list:
+        """Abort-mode run of all of target's samples in chunks, with the
+        cross-rank early-stop flag (sharding.run_abort_chunks).  workspaces:
+        one per chunk (grown as needed).  Returns the (offset, count) chunks."""
+        from . import sharding
+        parts = sharding.chunks(target.shape[0], chunk_samples)
+        while len(workspaces) < len(parts):
+            workspaces.append(self.new_workspace())
+
+        def one(k, off, n):
+            self.launch(target, diff, r, abort=True, stream=stream, workspace=workspaces[k], sample_offset=off,
+                        num_samples=n)
+        sharding.run_abort_chunks(one, r.found, target.shape[0], chunk_samples, group=group)
+        return parts
+
+    def read_timestamps(self, workspace: torch.Tensor | None = None):
+        """(start_ticks, found_ticks, tick_hz) of the last launch on workspace."""
+        a, b, hz = C.c_uint64(0), C.c_uint64(0), C.c_double(0.0)
+        ws = workspace if workspace is not None else self.workspace
+        _abi.check(self.L.hc_trifocal_read_timestamps(C.c_void_p(ws.data_ptr()), C.byref(a), C.byref(b), C.byref(hz)),
+                   "hc_trifocal_read_timestamps")
+        return a.value, b.value, hz.value
 
     def track(self, target: np.ndarray, diff: np.ndarray, abort: bool = False, stats: bool = True) -> TrackResult:
         """Synchronous convenience wrapper: H2D params, reset tracks, launch, sync."""
