@@ -10,9 +10,11 @@
 //    row (+ rhs + rowid) into a per-half buffer with ds_write_b128 and every
 //    lane reads it back with broadcast ds_read_b128 -- K/2 + K/2 LDS
 //    instructions per step instead of 2K ds_bpermute;
-//  * the cuCdivf factors of position i are parked in LDS by the pivot lane
-//    (no per-lane select bookkeeping), and since the lane with final rowid i
-//    owns position i, the back substitution needs no permutation array;
+//  * the lane with final rowid i owns position i and still holds pivot i in
+//    rA[i]: the back substitution recomputes its cuCdivf factors there (no
+//    factor storage, no permutation array);
+//  * the half-wave max of the pivot search ends with v_permlane16_swap (VALU)
+//    instead of an LDS swizzle;
 //  * 1/s and 1/s2 use v_rcp_f32 + one Newton step when s is in [2^-90, 2^120)
 //    (exhaustively verified correctly rounded there), the IEEE '/' otherwise;
 //  * cuCdivf(1, y) is evaluated as ((o1*brs)*o2, -(o1*bis)*o2), which equals
@@ -31,7 +33,6 @@ typedef float f2v __attribute__((ext_vector_type(2)));
 
 struct alignas(16) LUBuf {
     cf row[32];    // current pivot row: [0..29] A, [30] rhs, [31].x = rowid (int bits); reused for x in the back sub
-    divf f[32];    // cuCdivf factors of position i
 };
 static_assert(sizeof(divf) == 16, "divf layout");
 static_assert(sizeof(LUBuf) <= sizeof(cf) * NV * 7, "LUBuf must fit in SlotLDS::ent");
@@ -49,6 +50,15 @@ __device__ __forceinline__ float rcp_rn(float s) {
     return __builtin_fmaf(e0, r0, r0);
 }
 __device__ __forceinline__ bool rcp_fast_ok(float s) { return s >= 0x1p-90f && s < 0x1p+120f; }
+// cuCdivf factors of y with s = |y.re| + |y.im| in the fast range (== cdiv_factors(y))
+__device__ __forceinline__ divf cdiv_factors_fast(cf y, float s) {
+    divf f;
+    f.o1 = rcp_rn(s);
+    f.brs = y.x * f.o1;
+    f.bis = y.y * f.o1;
+    f.o2 = rcp_rn((f.brs * f.brs) + (f.bis * f.bis));   // argument in [0.5, 1]
+    return f;
+}
 
 __device__ __forceinline__ void st4(cf *p, cf a, cf b) {
     f4v v = {a.x, a.y, b.x, b.y};
@@ -58,6 +68,17 @@ __device__ __forceinline__ void ld4(const cf *p, cf &a, cf &b) {
     const f4v v = *reinterpret_cast<const f4v *>(p);
     a = cmk(v.x, v.y);
     b = cmk(v.z, v.w);
+}
+
+// max over each 32-lane half: DPP inside 16-lane rows, then v_permlane16_swap
+// across the row pair (VALU; no LDS round trip unlike ds_swizzle)
+__device__ __forceinline__ int half_max_int_p16(int v) {
+    v = max(v, dpp_i<DPP_QP_1032>(v));
+    v = max(v, dpp_i<DPP_QP_2301>(v));
+    v = max(v, dpp_i<DPP_ROW_HALF_MIRROR>(v));
+    v = max(v, dpp_i<DPP_ROW_MIRROR>(v));
+    const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return max((int)sw[0], (int)sw[1]);
 }
 
 // pivot lane: row elements J.. of the register row into the buffer
@@ -74,16 +95,17 @@ __device__ __forceinline__ void lu3_put_row(const cf (&rA)[NV], LUBuf &L) {
     }
 }
 
-// a_j -= l * u_j for j in [J0, NV), u from the broadcast buffer
-template <int J0>
+// a_j -= l * u_j for j in [J0, JE), u from the broadcast buffer
+template <int J0, int JE = NV>
 __device__ __forceinline__ void lu3_update(cf (&rA)[NV], const cf &l, bool below, const LUBuf &L) {
-    if constexpr (J0 < NV) {
-        if constexpr (J0 & 1) {
+    if constexpr (J0 < JE) {
+        if constexpr ((J0 & 1) || J0 + 1 >= JE) {
             const cf u = L.row[J0];
             if (below) rA[J0] = cmsub(rA[J0], l, u);
-            lu3_update<J0 + 1>(rA, l, below, L);
+            lu3_update<J0 + 1, JE>(rA, l, below, L);
         } else {
-            constexpr int N = (NV - J0) < LU3_CHUNK ? (NV - J0) : LU3_CHUNK;
+            constexpr int N0 = (JE - J0) < LU3_CHUNK ? (JE - J0) : LU3_CHUNK;
+            constexpr int N = N0 & ~1;
             cf u[N];
 #pragma unroll
             for (int q = 0; q < N; q += 2) ld4(&L.row[J0 + q], u[q], u[q + 1]);
@@ -92,7 +114,7 @@ __device__ __forceinline__ void lu3_update(cf (&rA)[NV], const cf &l, bool below
                 for (int q = 0; q < N; q++) rA[J0 + q] = cmsub(rA[J0 + q], l, u[q]);
             }
             __builtin_amdgcn_sched_barrier(0);
-            lu3_update<J0 + N>(rA, l, below, L);
+            lu3_update<J0 + N, JE>(rA, l, below, L);
         }
     }
 }
@@ -105,7 +127,7 @@ __device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, in
         const bool elig = rowid >= I && row_lane;
         const bool isn = v != v;
         const int key = (elig && !isn) ? __float_as_int(v) : -1;   // |.|+|.| >= +0: bits order like ints
-        const int mx = half_max_int(key);
+        const int mx = half_max_int_p16(key);
         // key == mx alone marks the candidates: mx >= 0 unless every eligible entry is
         // NaN, and then position I is NaN too (rare path).  Single compares ballot
         // straight into SGPRs (an && chain would be materialised first).
@@ -142,23 +164,17 @@ __device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, in
         const int piv_pos = __float_as_int(pr.x);
         if (is_piv) rowid = I;                                 // :70-82
         else if (rowid == I) rowid = piv_pos;
-        // cuCdivf factors of the pivot (:84)
-        divf f;
+        // 1 / pivot as cuCdivf(1, pivot) (:84); the back substitution recomputes the
+        // same factors from the pivot element its owner lane still holds
         cf reg;
         const float s = __builtin_fabsf(sxi.x) + __builtin_fabsf(sxi.y);   // == piv_abs
         if (__builtin_expect(__builtin_amdgcn_ballot_w64(!rcp_fast_ok(s)) == 0ull, 1)) {
-            // s in [2^-90, 2^120): non-zero, finite pivot
-            f.o1 = rcp_rn(s);
-            f.brs = sxi.x * f.o1;
-            f.bis = sxi.y * f.o1;
-            const float s2 = (f.brs * f.brs) + (f.bis * f.bis);   // in [0.5, 1]
-            f.o2 = rcp_rn(s2);
+            const divf f = cdiv_factors_fast(sxi, s);          // s in [2^-90, 2^120): non-zero, finite
             reg = cmk((f.o1 * f.brs) * f.o2, (-(f.o1 * f.bis)) * f.o2);
         } else {
-            f = cdiv_factors(sxi);
+            const divf f = cdiv_factors(sxi);
             reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
         }
-        if (is_piv) *reinterpret_cast<f4v *>(&L.f[I]) = f4v{f.o1, f.brs, f.bis, f.o2};
         const bool below = rowid > I;                          // :86-93
         cf l = cmk(0.0f, 0.0f);
         if (below) {
@@ -173,17 +189,27 @@ __device__ __forceinline__ void lu3_forward(cf (&rA)[NV], cf &rB, int &rowid, in
     }
 }
 
-// back substitution (:97-106): the lane with rowid == I owns position I and
-// its factors; it computes x_I and publishes it in row[I]
+// back substitution (:97-106): the lane with final rowid == I owns position I;
+// its rA[I] is still the pivot element of step I, so it recomputes that pivot's
+// cuCdivf factors (same inputs, same ops as the forward step), computes x_I and
+// publishes it in row[I]
 template <int I>
-__device__ __forceinline__ void lu3_backward(const cf (&rA)[NV], cf &rB, int rowid, const divf &myf, LUBuf &L) {
+__device__ __forceinline__ void lu3_backward(const cf (&rA)[NV], cf &rB, int rowid, LUBuf &L) {
     if constexpr (I >= 0) {
-        const cf cand = cdiv_apply(rB, myf);
-        if (rowid == I) L.row[I] = cand;
+        const cf piv = rA[I];
+        const float s = __builtin_fabsf(piv.x) + __builtin_fabsf(piv.y);
+        const bool own = rowid == I;
+        divf f;
+        if (__builtin_expect((__builtin_amdgcn_ballot_w64(!rcp_fast_ok(s)) & __builtin_amdgcn_ballot_w64(own)) == 0ull, 1))
+            f = cdiv_factors_fast(piv, s);
+        else
+            f = cdiv_factors(piv);
+        const cf cand = cdiv_apply(rB, f);
+        if (own) L.row[I] = cand;
         wave_lds_sync();
         const cf xi = L.row[I];
         if (rowid < I) rB = cmsub(rB, xi, rA[I]);
-        lu3_backward<I - 1>(rA, rB, rowid, myf, L);
+        lu3_backward<I - 1>(rA, rB, rowid, L);
     }
 }
 
@@ -193,11 +219,7 @@ __device__ __forceinline__ cf lu_solve3(cf (&rA)[NV], cf rB, int lane, LUBuf &L)
     const bool row_lane = r < NV;
     int rowid = row_lane ? r : 99;   // padding lanes never pivot
     lu3_forward<0>(rA, rB, rowid, lane, r, hb, row_lane, L);
-    wave_lds_sync();
-    const f4v mf = *reinterpret_cast<const f4v *>(&L.f[row_lane ? rowid : 0]);
-    divf myf;
-    myf.o1 = mf.x; myf.brs = mf.y; myf.bis = mf.z; myf.o2 = mf.w;
-    lu3_backward<NV - 1>(rA, rB, rowid, myf, L);
+    lu3_backward<NV - 1>(rA, rB, rowid, L);
     wave_lds_sync();
     return L.row[row_lane ? r : 0];
 }
