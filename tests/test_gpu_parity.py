@@ -195,3 +195,26 @@ def test_tracker_abort_chunked(problem, samples100, tracker):
     stamps = [tracker.read_timestamps(w)[:2] for w in wss]
     hz = tracker.read_timestamps(wss[0])[2]
     assert sharding.first_found_seconds(stamps, hz) > 0
+
+
+@pytest.mark.gpu
+def test_cli_config2_matches_golden(tmp_path):
+    """bin/magmaHC-main (C++ GPU_HC_Solver over the C-ABI) on config 2: the
+    solution statistics it writes equal the golden run's counts."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "trifocal_pose_estimation_using_improved_gpuhc_amd", "bin", "magmaHC-main")
+    assert os.path.exists(cli), "CLI not built"
+    shutil.copytree(os.path.join(root, "data"), os.path.join(tmp_path, "data"))
+    out = subprocess.run([cli, "-p", "trifocal_2op1p_30x30", "-d", str(tmp_path)], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    stats = open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Sols_Statistics.txt")).read().split()
+    assert [int(v) for v in stats[:3]] == [int(v) for v in g["counts"]]
+    assert float(open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Timings.txt")).read().split()[0]) > 0
+    # abort mode (config 3 semantics through the CLI)
+    out = subprocess.run([cli, "-p", "trifocal_2op1p_30x30", "-d", str(tmp_path), "-n", "1000", "--abort"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr

@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <filesystem>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -473,7 +474,10 @@ bool run_GPU_HC_Solver(const HC_Settings &settings, const std::string &root_dir,
     printf(" - [Std dev GPU Computation Time] %7.2f (ms)\n", sigma);
     std::string root = root_dir;
     if (!root.empty() && root.back() != '/') root += '/';
+    std::error_code ec;
+    std::filesystem::create_directories(root + "Output_Write_Files", ec);
     std::ofstream tf(root + "Output_Write_Files/GPU_Timings.txt");
+    if (!tf) std::cerr << "cannot write " << root << "Output_Write_Files/GPU_Timings.txt" << std::endl;
     for (double v : all_ms) tf << v << "\n";
     // reference file columns: converged, "inf" (holds real), "real" (holds inf) -- written
     // here with the same byte layout: converged \t real \t inf (cmd/magmaHC-main.cpp:107-116)
