@@ -1085,8 +1085,8 @@ const char *hc_trifocal_version(void) {
     case 1: return "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
     case 2: return "hc_trifocal gfx950 v2 (2 paths/wave, bpermute LU, per-lane term lists)";
     default:
-        return hc::v3_minwaves() == 4 ? "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, packed evals, 4 waves/SIMD)"
-                                      : "hc_trifocal gfx950 v3 (2 paths/wave, LDS-broadcast LU, packed evals, 3 waves/SIMD)";
+        return hc::v3_minwaves() == 4 ? "hc_trifocal gfx950 v3.1 (2 paths/wave, LDS-broadcast LU, permlane16 pivot search, packed evals, 4 waves/SIMD)"
+                                      : "hc_trifocal gfx950 v3.1 (2 paths/wave, LDS-broadcast LU, permlane16 pivot search, packed evals, 3 waves/SIMD)";
     }
 }
 
