@@ -16,6 +16,7 @@
 #include <string>
 #include <vector>
 
+#include "hc_pose.h"
 #include "hc_trifocal.h"
 
 #define MAX_NUM_OF_GPUS 8   // definitions.hpp:8
@@ -46,6 +47,19 @@ public:
     double transfer_d2h_time[MAX_NUM_OF_GPUS] = {0.0};
     double multi_GPUs_time = 0.0;
     double first_good_pose_time[MAX_NUM_OF_GPUS] = {0.0};   // abort mode, device clock (s), <0: none
+    double pose_time = 0.0;   // device pose recovery + maximal support, all GPUs (s)
+
+    // maximal-support pose of the last run (Evaluations.cpp:298-543 on the device,
+    // include/hc_pose.h) and its error against GT_Poses21/31 of the data index
+    hcPoseSelection pose_selection{};
+    float pose_residuals[4] = {-1.0f, -1.0f, -1.0f, -1.0f};   // rot21, rot31 (rad), transl21, transl31
+    bool pose_success = false;
+    struct PoseRecord {
+        int success = 0;
+        float residuals[4] = {-1.0f, -1.0f, -1.0f, -1.0f};
+        int path21 = -1, path31 = -1, num_candidates = 0;
+    };
+    std::vector<PoseRecord> Collect_Pose;   // one per Solve_by_GPU_HC
 
     explicit GPU_HC_Solver(const HC_Settings &settings, const std::string &root_dir = "../../");
     ~GPU_HC_Solver();
@@ -87,6 +101,7 @@ private:
     int GPUHC_Max_Steps = 80, GPUHC_Max_Correction_Steps = 3, GPUHC_delta_t_incremental_steps = 4;
     int Num_Of_Vars = 30, Num_Of_Params = 33, Num_Of_Tracks = 312;
     bool Abort_RANSAC_by_Good_Sol = false;
+    int Pose_Flags = 0;   // Pose_Selection_Reference_Quirks -> HC_POSE_REFERENCE_QUIRKS
     int Num_Of_GPUs = 1;
     int Num_Of_RANSAC_Iterations = 100;   // NUM_OF_RANSAC_ITERATIONS (definitions.hpp:12), runtime here
     int sub_RANSAC_iters[MAX_NUM_OF_GPUS] = {0};

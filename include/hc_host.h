@@ -10,6 +10,7 @@
  *                             (magmaHC/GPU_HC_Solver.cpp:252-306), glibc srand/rand
  *   hc_split_samples          GPU_HC_Solver ctor sample split (GPU_HC_Solver.cpp:85-88)
  *   hc_count_solutions        Evaluations::Evaluate_HC_Sols (magmaHC/Evaluations.cpp:145-182)
+ *   hc_write_converged_sols   Evaluations::Write_Converged_Sols (magmaHC/Evaluations.cpp:120-143)
  * All complex arrays are interleaved float (re, im) == hcComplex.
  */
 #ifndef HC_HOST_H
@@ -43,6 +44,13 @@ void hc_prepare_target_params(unsigned seed, int num_gpus, const int *sub_ransac
 /* counts[0] converged, counts[1] real (converged, all |Im| <= 1e-4), counts[2] inf. */
 void hc_count_solutions(int num_samples, const float *tracks /* 312N x 31 x 2 */,
                         const uint8_t *converge, const uint8_t *infinity, int32_t *counts);
+
+/* Writes <file> in the byte layout of Evaluations::Write_Converged_Sols: per
+   sample a "---- RANSAC Iteration k ----" header, then for every converged
+   path its global batch id and 30 "re\tim" lines (std::setprecision(20)).
+   Returns the number of paths written, <0 if the file cannot be opened. */
+int hc_write_converged_sols(const char *file, int num_samples, const float *tracks /* 312N x 31 x 2 */,
+                            const uint8_t *converge);
 
 #ifdef __cplusplus
 }

@@ -518,6 +518,185 @@ int orc_score_hypothesis(const float *xf, int E, const float *loc, const float *
 }
 
 /* ====================================================================== */
+/* Pose recovery + maximal-support selection:       */
+/* Evaluations::Transform_GPUHC_Sols_to_Trifocal_Relative_Pose            */
+/* (Evaluations.cpp:298-358), get_Solution_with_Maximal_Support (:382-504) */
+/* and the util.hpp helpers they call, written in the reference's own      */
+/* structure: a candidate list in batch-id order, then a loop over         */
+/* candidates x edgels with the running ">=" maximum.                      */
+/* ====================================================================== */
+/* util.hpp:104-112 get_Matrix_Vector_Product<3> (accumulates from 0.0)   */
+static void u_matvec(const float *M, const float *V, float *MV) {
+    for (int i = 0; i < 3; i++) {
+        MV[i] = 0.0f;
+        for (int j = 0; j < 3; j++) MV[i] += M[i * 3 + j] * V[j];
+    }
+}
+/* util.hpp:114-124 get_Matrix_Transpose<3> (in place)                    */
+static void u_transpose(float *R) {
+    float T[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) T[i * 3 + j] = R[j * 3 + i];
+    for (int i = 0; i < 9; i++) R[i] = T[i];
+}
+/* util.hpp:76-78 get_Vector_Norm                                         */
+static float u_norm(const float *v) { return sqrtf(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+/* util.hpp:69-74 Normalize_Translation_Vector                            */
+static void u_normalize_t(float *t) {
+    const float n = u_norm(t);
+    t[0] /= n; t[1] /= n; t[2] /= n;
+}
+/* util.hpp:31-66 Cayley_To_Rotation_Matrix + Normalize_Rotation_Matrix   */
+static void u_cayley(const float *r, float *R) {
+    R[0] = 1 + r[0] * r[0] - (r[1] * r[1] + r[2] * r[2]);
+    R[1] = 2 * (r[0] * r[1] - r[2]);
+    R[2] = 2 * (r[0] * r[2] + r[1]);
+    R[3] = 2 * (r[0] * r[1] + r[2]);
+    R[4] = 1 + r[1] * r[1] - (r[0] * r[0] + r[2] * r[2]);
+    R[5] = 2 * (r[1] * r[2] - r[0]);
+    R[6] = 2 * (r[0] * r[2] - r[1]);
+    R[7] = 2 * (r[1] * r[2] + r[0]);
+    R[8] = 1 + r[2] * r[2] - (r[0] * r[0] + r[1] * r[1]);
+    const float n1 = sqrtf(R[0] * R[0] + R[3] * R[3] + R[6] * R[6]);
+    const float n2 = sqrtf(R[1] * R[1] + R[4] * R[4] + R[7] * R[7]);
+    const float n3 = sqrtf(R[2] * R[2] + R[5] * R[5] + R[8] * R[8]);
+    R[0] /= n1; R[3] /= n1; R[6] /= n1;
+    R[1] /= n2; R[4] /= n2; R[7] /= n2;
+    R[2] /= n3; R[5] /= n3; R[8] /= n3;
+}
+/* util.hpp:169-186 get_depth_rho                                         */
+static float u_depth_rho(const float *g1, const float *g2, float *R, const float *T) {
+    float mvp[3], Rg2[3], rho;
+    u_transpose(R);
+    u_matvec(R, g2, mvp);
+    for (int i = 0; i < 3; i++) Rg2[i] = mvp[i];
+    rho = T[2] * Rg2[2];
+    u_matvec(R, T, mvp);
+    rho -= mvp[2];
+    u_transpose(R);
+    u_matvec(R, g1, mvp);
+    rho /= (float)(1 - mvp[2] * Rg2[2]);
+    return rho;
+}
+/* util.hpp:188-209 get_Reprojection_Pixels_Error (gamma2 scaled in place) */
+static float u_reproj_px(const float *g1, float *g2, const float *R, const float *T, const float *K, float rho1) {
+    float mvp[3];
+    u_matvec(R, g1, mvp);
+    for (int i = 0; i < 3; i++) { mvp[i] *= rho1; mvp[i] += T[i]; }
+    mvp[0] /= mvp[2];
+    mvp[1] /= mvp[2];
+    mvp[0] = mvp[0] * K[0] + K[2];
+    mvp[1] = mvp[1] * K[4] + K[5];
+    g2[0] = g2[0] * K[0] + K[2];
+    g2[1] = g2[1] * K[4] + K[5];
+    mvp[0] -= g2[0];
+    mvp[1] -= g2[1];
+    mvp[2] = 0.0f;
+    return u_norm(mvp);
+}
+
+typedef struct { float R21[9], t21[3], R31[9], t31[3]; } orc_pose;
+
+/* Evaluations.cpp:235-265 from the 31-complex track x                    */
+static void convert_pose(const float *x, orc_pose *P) {
+    for (int i = 0; i < 3; i++) { P->t21[i] = x[2 * (18 + i)]; P->t31[i] = x[2 * (21 + i)]; }
+    u_normalize_t(P->t21);
+    u_normalize_t(P->t31);
+    float r[3];
+    for (int i = 0; i < 3; i++) r[i] = x[2 * (24 + i)];
+    u_cayley(r, P->R21);
+    for (int i = 0; i < 3; i++) r[i] = x[2 * (27 + i)];
+    u_cayley(r, P->R31);
+}
+
+int orc_pose_support(int num_paths, const float *tracks, const uint8_t *conv, int E, const float *loc,
+                     const float *K, int quirks, int32_t *inliers, orc_pose_selection *sel) {
+    /* ---- Transform_GPUHC_Sols_to_Trifocal_Relative_Pose (:298-358) ---- */
+    int *cand = (int *)malloc(sizeof(int) * (size_t)(num_paths > 0 ? num_paths : 1));
+    orc_pose *poses = (orc_pose *)malloc(sizeof(orc_pose) * (size_t)(num_paths > 0 ? num_paths : 1));
+    int nc = 0;
+    for (int bs = 0; bs < num_paths; bs++) {
+        inliers[2 * bs] = inliers[2 * bs + 1] = -1;
+        const int r = bs / ORC_NTRACK;
+        const long ci = quirks ? (long)ORC_NTRACK * r + bs : bs;          /* :317 */
+        if (ci >= num_paths || !conv[ci]) continue;
+        const float *x = tracks + (size_t)bs * (ORC_NV + 1) * 2;
+        int small_imag = 0, pos_depth = 0;
+        for (int vi = 0; vi < 6; vi++)                                    /* :324-327 */
+            if ((double)fabsf(x[2 * (24 + vi) + 1]) < 1e-5) small_imag++;
+        if (small_imag < 6) continue;
+        for (int di = 0; di < 8; di++)                                    /* :330-332 */
+            if (x[2 * di] >= 0) pos_depth++;
+        if (pos_depth < 8) continue;
+        convert_pose(quirks ? tracks : x, &poses[nc]);                    /* :334-341 */
+        cand[nc++] = bs;
+    }
+    /* ---- get_Solution_with_Maximal_Support (:382-504) ---- */
+    int max21 = 0, max31 = 0, pick21 = -1, pick31 = -1;
+    for (int cp = 0; cp < nc; cp++) {
+        int n21 = 0, n31 = 0;
+        orc_pose *P = &poses[cp];
+        for (int ei = 0; ei < E; ei++) {
+            float g1[3] = {loc[ei * 6 + 0], loc[ei * 6 + 1], 1.0f};
+            float g2[3] = {loc[ei * 6 + 2], loc[ei * 6 + 3], 1.0f};
+            float g3[3] = {loc[ei * 6 + 4], loc[ei * 6 + 5], 1.0f};
+            const float rho21 = u_depth_rho(g1, g2, P->R21, P->t21);
+            const float e21 = u_reproj_px(g1, g2, P->R21, P->t21, K, rho21);
+            const float rho31 = u_depth_rho(g1, g3, P->R31, P->t31);
+            const float e31 = u_reproj_px(g1, g3, P->R31, P->t31, K, rho31);
+            if (e21 < 2) n21++;                                           /* REPROJ_ERROR_INLIER_THRESH */
+            if (e31 < 2) n31++;
+        }
+        inliers[2 * cand[cp]] = n21;
+        inliers[2 * cand[cp] + 1] = n31;
+        /* :455-467: push when >= the running max; the reference then reads element
+           [0] (quirks), its commented-out rule keeps the latest one (default) */
+        if (n21 >= max21) { max21 = n21; if (!quirks || pick21 < 0) pick21 = cp; }
+        if (n31 >= max31) { max31 = n31; if (!quirks || pick31 < 0) pick31 = cp; }
+    }
+    memset(sel, 0, sizeof(*sel));
+    sel->num_candidates = nc;
+    sel->path21 = pick21 >= 0 ? cand[pick21] : -1;
+    sel->path31 = pick31 >= 0 ? cand[pick31] : -1;
+    sel->inliers21 = pick21 >= 0 ? inliers[2 * cand[pick21]] : -1;
+    sel->inliers31 = pick31 >= 0 ? inliers[2 * cand[pick31] + 1] : -1;
+    if (pick21 >= 0) { memcpy(sel->R21, poses[pick21].R21, 36); memcpy(sel->t21, poses[pick21].t21, 12); }
+    if (pick31 >= 0) { memcpy(sel->R31, poses[pick31].R31, 36); memcpy(sel->t31, poses[pick31].t31, 12); }
+    free(cand);
+    free(poses);
+    return nc > 0;                                                       /* :490-503 */
+}
+
+/* Evaluations.cpp:360-380 + :523-543 (Measure_Relative_Pose_Error)       */
+static float rot_residual(const float *gt, const float *R) {
+    float G[9], M[9];
+    for (int i = 0; i < 9; i++) G[i] = gt[i];
+    u_transpose(G);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            M[i * 3 + j] = 0;
+            for (int k = 0; k < 3; k++) M[i * 3 + j] += G[i * 3 + k] * R[k * 3 + j];
+        }
+    float tr = 0.0f;
+    for (int i = 0; i < 3; i++) tr += M[i * 3 + i];
+    return (float)acos(0.5 * (tr - 1.0));
+}
+static float transl_residual(const float *gt_t, const float *t) {
+    float g[3] = {gt_t[0], gt_t[1], gt_t[2]};
+    u_normalize_t(g);
+    float dot = 0.0f;
+    for (int i = 0; i < 3; i++) dot += g[i] * t[i];
+    return (float)fabs(dot - 1.0);
+}
+int orc_pose_residuals(const float *gt21, const float *gt31, const orc_pose_selection *sel, float *out4) {
+    out4[0] = rot_residual(gt21, sel->R21);
+    out4[1] = rot_residual(gt31, sel->R31);
+    out4[2] = transl_residual(gt21 + 9, sel->t21);
+    out4[3] = transl_residual(gt31 + 9, sel->t31);
+    return out4[2] < 1e-1 && out4[3] < 1e-1 && out4[0] < 1e-1 && out4[1] < 1e-1;
+}
+
+/* ====================================================================== */
 /* LAPACK cgesv semantics (call sites CPUHC_Generic_Solver_Eval_by_Indx.cpp:93,100,107,114,127) */
 /* cgetf2 (right-looking, icamax on cabs1, first max) + cgetrs.  The       */
 /* OpenBLAS 0.3.23 kernels the reference links are not reproducible here:  */

@@ -120,6 +120,24 @@ double orc_cpuhc_track(const orc_hc_settings *s, int num_samples,
 void orc_count_solutions(int num_samples, const float *tracks, const uint8_t *conv,
                          const uint8_t *inf, int *out3);
 
+/* Pose recovery + maximal-support selection (Evaluations.cpp:298-504, util.hpp):
+   candidates = converged, |Im x[24..29]| < 1e-5, Re x[0..7] >= 0, in batch-id
+   order; inliers (2 per path, -1 for non-candidates); selection = last
+   candidate with the maximal count per view, or with quirks != 0 the
+   reference's literal behaviour (flag index b + 312*(b/312), pose of path 0,
+   list element [0]).  Returns 1 if there is a candidate. */
+typedef struct {
+    int32_t num_candidates, path21, inliers21, path31, inliers31, pad;
+    uint64_t key21, key31;                  /* unused by the oracle (0)       */
+    float R21[9], t21[3], R31[9], t31[3];
+} orc_pose_selection;                       /* == hcPoseSelection layout      */
+int orc_pose_support(int num_paths, const float *tracks, const uint8_t *conv, int num_edgels,
+                     const float *loc, const float *K, int quirks, int32_t *inliers,
+                     orc_pose_selection *sel);
+/* Measure_Relative_Pose_Error: out4 = rot res 21, 31, transl res 21, 31; 1 = success */
+int orc_pose_residuals(const float *gt_pose21, const float *gt_pose31, const orc_pose_selection *sel,
+                       float *out4);
+
 int orc_max_threads(void);
 
 #ifdef __cplusplus

@@ -195,3 +195,42 @@ def count_solutions(tracks, conv, inf):
     N = conv.shape[0] // NT
     lib().orc_count_solutions(C.c_int(N), _p(np.ascontiguousarray(tracks, np.float32)), _p(conv), _p(inf), _p(out))
     return tuple(int(v) for v in out)
+
+
+# ----------------------------------------------------------------- pose recovery (§8 f1)
+class PoseSelection(C.Structure):
+    """== orc_pose_selection == hcPoseSelection (include/hc_pose.h)."""
+    _fields_ = [("num_candidates", C.c_int32), ("path21", C.c_int32), ("inliers21", C.c_int32),
+                ("path31", C.c_int32), ("inliers31", C.c_int32), ("pad", C.c_int32),
+                ("key21", C.c_uint64), ("key31", C.c_uint64),
+                ("R21", C.c_float * 9), ("t21", C.c_float * 3), ("R31", C.c_float * 9), ("t31", C.c_float * 3)]
+
+
+def selection_dict(s) -> dict:
+    return dict(num_candidates=s.num_candidates, path21=s.path21, inliers21=s.inliers21, path31=s.path31,
+                inliers31=s.inliers31, R21=np.array(s.R21[:], np.float32), t21=np.array(s.t21[:], np.float32),
+                R31=np.array(s.R31[:], np.float32), t31=np.array(s.t31[:], np.float32))
+
+
+def pose_support(tracks, conv, loc, K, quirks=False):
+    """Evaluations.cpp:298-504 restated: returns (inliers (312N, 2) int32, selection dict)."""
+    tr = np.ascontiguousarray(tracks, np.float32)
+    cv = np.ascontiguousarray(conv, np.uint8)
+    n = cv.shape[0]
+    inl = np.zeros((n, 2), np.int32)
+    sel = PoseSelection()
+    lib().orc_pose_support(C.c_int(n), _p(tr), _p(cv), C.c_int(loc.shape[0]),
+                           _p(np.ascontiguousarray(loc, np.float32)), _p(np.ascontiguousarray(K, np.float32)),
+                           C.c_int(1 if quirks else 0), _p(inl), C.byref(sel))
+    return inl, selection_dict(sel)
+
+
+def pose_residuals(gt21, gt31, sel: dict):
+    """Measure_Relative_Pose_Error: ([rot21, rot31, transl21, transl31], success)."""
+    s = PoseSelection()
+    for k in ("R21", "t21", "R31", "t31"):
+        getattr(s, k)[:] = [float(v) for v in sel[k]]
+    out = np.zeros(4, np.float32)
+    ok = lib().orc_pose_residuals(_p(np.ascontiguousarray(gt21, np.float32)),
+                                  _p(np.ascontiguousarray(gt31, np.float32)), C.byref(s), _p(out))
+    return out, bool(ok)

@@ -10,8 +10,11 @@ outputs pin the oracle so later rounds (and the GPU box, which has no
                         hypothesis-scoring results of every converged path
   cpuhc_seed0.npz       CPU-HC semantics: counts for 100 samples + flags/hashes of samples 0..1
   kat_eval.npz          one evaluation point: x, p, d -> dH/dx, dH/dt, H and the LU solve
+  pose_N100_seed0.npz   pose recovery / maximal support over the GPU-HC tracks of
+                        the 100 samples: the candidate paths' tracks, their inlier counts, the
+                        selected path / inliers / pose per view and its GT residuals
 
-Run:  python tests/golden/make_golden.py      (takes ~1-2 min on 8 cores)
+Run:  python tests/golden/make_golden.py [--only pose]   (takes ~1-2 min on 8 cores)
 """
 import os
 import sys
@@ -43,15 +46,36 @@ def track_hash(tracks):
     return h
 
 
+def pose_fixture(tr, conv, loc, K):
+    gt21 = O.read_floats(os.path.join(RANS, "GT_Poses21", "GT_Poses21_000.txt"), 12)
+    gt31 = O.read_floats(os.path.join(RANS, "GT_Poses31", "GT_Poses31_000.txt"), 12)
+    inl, sel = O.pose_support(tr, conv, loc, K)
+    ids = np.nonzero(inl[:, 0] >= 0)[0].astype(np.int32)
+    res, ok = O.pose_residuals(gt21, gt31, sel)
+    np.savez_compressed(os.path.join(HERE, "pose_N100_seed0.npz"), cand_ids=ids, cand_tracks=tr[ids],
+                        cand_inliers=inl[ids], num_candidates=np.int32(sel["num_candidates"]),
+                        path=np.array([sel["path21"], sel["path31"]], np.int32),
+                        inliers=np.array([sel["inliers21"], sel["inliers31"]], np.int32),
+                        R21=sel["R21"], t21=sel["t21"], R31=sel["R31"], t31=sel["t31"], residuals=res,
+                        success=np.bool_(ok))
+    print("pose: candidates", sel["num_candidates"], "paths", sel["path21"], sel["path31"], "residuals", res, ok)
+
+
 def main():
+    only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ss, sp, dhdx, dhdt = O.read_problem(PROB)
     U = np.concatenate([dhdx, dhdt]).astype(np.int32)
     loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", "Triplet_Edgels_000.txt"))
     K = O.read_floats(os.path.join(RANS, "Intrinsic_Matrix.txt"), 9)
     tgt, dif, picked = O.prepare_target_params(0, [100], loc, tan, sp)
+    if only == "pose":
+        tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
+        pose_fixture(tr, conv, loc, K)
+        return
     np.savez_compressed(os.path.join(HERE, "samples_seed0.npz"), picked=picked, target=tgt, diff=dif)
 
     tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
+    pose_fixture(tr, conv, loc, K)
     conv_ids = np.nonzero(conv)[0]
     scores = np.array([O.score_hypothesis(tr[b], loc, K) for b in conv_ids], dtype=np.int64).reshape(-1, 3)
     np.savez_compressed(os.path.join(HERE, "gpuhc_N100_seed0.npz"),

@@ -30,9 +30,18 @@ def _declared_c_functions(header):
     return set(names)
 
 
+def _all_declared():
+    """Every function the public headers declare (include/*.h)."""
+    names = set()
+    for h in sorted(os.listdir(INCLUDE)):
+        if h.endswith(".h"):
+            names |= _declared_c_functions(h)
+    return names
+
+
 def test_headers_declare_the_bound_symbols():
     from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
-    declared = _declared_c_functions("hc_trifocal.h") | _declared_c_functions("hc_host.h")
+    declared = _all_declared()
     assert declared == set(_abi.DECLARED_SYMBOLS)
 
 
@@ -41,7 +50,7 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _abi.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
     exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
-    declared = _declared_c_functions("hc_trifocal.h") | _declared_c_functions("hc_host.h")
+    declared = _all_declared()
     missing = declared - exported
     assert not missing, f"declared but not exported: {sorted(missing)}"
     L = _abi.lib()
@@ -175,3 +184,35 @@ def test_count_solutions_matches_oracle(oracle):
     inf = ((rng.random(312 * n) < 0.2) & (conv == 0)).astype(np.uint8)
     assert count_solutions(tracks, conv, inf) == tuple(oracle.count_solutions(tracks, conv, inf))
     assert count_solutions(tracks, np.zeros_like(conv), np.zeros_like(inf)) == (0, 0, 0)
+
+
+def test_write_converged_sols_layout(tmp_path):
+    """hc_write_converged_sols == Evaluations::Write_Converged_Sols byte layout
+    (Evaluations.cpp:120-143): header per sample, global batch id, 30 re/im lines
+    printed with std::setprecision(20) (== printf %.20g of the float)."""
+    import ctypes as C
+
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+    rng = np.random.default_rng(3)
+    N = 2
+    tr = rng.standard_normal((312 * N, 31, 2)).astype(np.float32)
+    tr[5, 3, 0] = 0.0
+    tr[7, 4, 1] = -0.0
+    tr[9, 1, 0] = 1e-30
+    conv = (rng.random(312 * N) < 0.1).astype(np.uint8)
+    f = str(tmp_path / "sols.txt")
+    n = _abi.lib().hc_write_converged_sols(f.encode(), C.c_int(N), C.c_void_p(tr.ctypes.data),
+                                           C.c_void_p(conv.ctypes.data))
+    assert n == int(conv.sum())
+    exp = []
+    for ri in range(N):
+        exp.append(f"-------------------- RANSAC Iteration {ri + 1} --------------------\n\n")
+        for bs in range(312):
+            b = ri * 312 + bs
+            if conv[b]:
+                exp.append(f"{b}\n")
+                for v in range(30):
+                    exp.append(f"{float(tr[b, v, 0]):.20g}\t{float(tr[b, v, 1]):.20g}\n")
+                exp.append("\n")
+        exp.append("\n")
+    assert open(f).read() == "".join(exp)

@@ -214,6 +214,11 @@ def test_cli_config2_matches_golden(tmp_path):
     stats = open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Sols_Statistics.txt")).read().split()
     assert [int(v) for v in stats[:3]] == [int(v) for v in g["counts"]]
     assert float(open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Timings.txt")).read().split()[0]) > 0
+    # device pose recovery: the maximal-support pose matches GT_Poses*_000
+    pr = open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Pose_Results.txt")).read().split()
+    gp = np.load(os.path.join(GOLDEN, "pose_N100_seed0.npz"))
+    assert int(pr[0]) == 1 and [int(pr[5]), int(pr[6])] == gp["path"].tolist() and int(pr[7]) == int(gp["num_candidates"])
+    assert max(float(v) for v in pr[1:5]) < 1e-3
     # abort mode (config 3 semantics through the CLI)
     out = subprocess.run([cli, "-p", "trifocal_2op1p_30x30", "-d", str(tmp_path), "-n", "1000", "--abort"],
                          capture_output=True, text=True, timeout=300)

@@ -44,6 +44,18 @@ class hcTrackArgs(C.Structure):
                 ("stats", C.c_void_p)]
 
 
+class hcPoseSelection(C.Structure):
+    """include/hc_pose.h"""
+    _fields_ = [("num_candidates", C.c_int32), ("path21", C.c_int32), ("inliers21", C.c_int32),
+                ("path31", C.c_int32), ("inliers31", C.c_int32), ("pad", C.c_int32),
+                ("key21", C.c_uint64), ("key31", C.c_uint64),
+                ("R21", C.c_float * 9), ("t21", C.c_float * 3), ("R31", C.c_float * 9), ("t31", C.c_float * 3)]
+
+
+POSE_SELECTION_BYTES = C.sizeof(hcPoseSelection)
+HC_POSE_REFERENCE_QUIRKS = 1
+
+
 class hcAbortArgs(C.Structure):
     _fields_ = [("num_triplet_edgels", C.c_int),
                 ("triplet_edge_locations", C.c_void_p),
@@ -83,6 +95,15 @@ def lib() -> C.CDLL:
         L.hc_trifocal_eval_batched.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                                C.c_void_p]
+        L.hc_trifocal_pose_support.restype = C.c_int
+        L.hc_trifocal_pose_support.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                               C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.hc_pose_merge.restype = None
+        L.hc_pose_merge.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(hcPoseSelection)]
+        L.hc_pose_residuals.restype = C.c_int
+        L.hc_pose_residuals.argtypes = [C.c_void_p] * 6 + [C.c_void_p]
+        L.hc_write_converged_sols.restype = C.c_int
+        L.hc_write_converged_sols.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]
         L.hc_prepare_target_params.argtypes = [C.c_uint, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
                                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
         for fn in ("hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
@@ -106,4 +127,5 @@ DECLARED_SYMBOLS = (
     "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
     "hc_count_triplet_edgels", "hc_read_triplet_edgels", "hc_split_samples", "hc_prepare_target_params",
     "hc_count_solutions",
+    "hc_trifocal_pose_support", "hc_pose_merge", "hc_pose_residuals", "hc_write_converged_sols",
 )

@@ -91,6 +91,11 @@ struct GPU_HC_Solver::PerGPU {
     float *d_edgels = nullptr, *d_K = nullptr;
     uint8_t *d_found = nullptr;
     int32_t *d_batch_index = nullptr;
+    // pose recovery / maximal support (hc_pose.h), every run
+    int32_t *d_inliers = nullptr;
+    hcPoseSelection *d_sel = nullptr;
+    hcPoseSelection h_sel{};
+    int edgel_capacity = 0;
     std::vector<hcComplex> h_track;
     std::vector<uint8_t> h_conv, h_inf;
     std::vector<hcPathStats> h_stats;
@@ -112,6 +117,7 @@ GPU_HC_Solver::GPU_HC_Solver(const HC_Settings &S, const std::string &root_dir) 
     RANSAC_Dataset_Name = S.has("RANSAC_Dataset") ? S.str("RANSAC_Dataset") : "Synthetic";
     Num_Of_GPUs = S.i("Num_Of_GPUs", 1);
     Num_Of_RANSAC_Iterations = S.i("Num_Of_RANSAC_Iterations", 100);
+    Pose_Flags = S.b("Pose_Selection_Reference_Quirks", false) ? HC_POSE_REFERENCE_QUIRKS : 0;
     if (HC_problem != "trifocal_2op1p_30x30" || Num_Of_Vars != NV || Num_Of_Params != NPP - 1 || Num_Of_Tracks != NT)
         throw std::runtime_error("this build implements trifocal_2op1p_30x30 (30 vars, 33 params, 312 tracks) only");
     int device_count = 0;
@@ -165,6 +171,8 @@ void GPU_HC_Solver::Allocate_Arrays() {
         HC_HIP_CHECK(hipMalloc(&p->d_inf, std::max<size_t>(1, n)));
         HC_HIP_CHECK(hipMalloc(&p->d_stats, std::max<size_t>(1, n) * sizeof(hcPathStats)));
         HC_HIP_CHECK(hipMalloc(&p->d_ws, wsb));
+        HC_HIP_CHECK(hipMalloc(&p->d_inliers, std::max<size_t>(1, n) * 2 * sizeof(int32_t)));
+        HC_HIP_CHECK(hipMalloc(&p->d_sel, sizeof(hcPoseSelection)));
         p->ws_bytes = wsb;
         p->h_track.resize(n * (NV + 1));
         p->h_conv.resize(n);
@@ -235,8 +243,6 @@ void GPU_HC_Solver::Set_RANSAC_Abort_Arrays() {
     for (PerGPU *p : gpus_) {
         HC_HIP_CHECK(hipSetDevice(p->dev));
         const size_t n = (size_t)NT * p->N;
-        HC_HIP_CHECK(hipMalloc(&p->d_edgels, (size_t)Num_Of_Triplet_Edgels * 6 * sizeof(float)));
-        HC_HIP_CHECK(hipMalloc(&p->d_K, 9 * sizeof(float)));
         HC_HIP_CHECK(hipMalloc(&p->d_found, 1));
         HC_HIP_CHECK(hipMalloc(&p->d_batch_index, std::max<size_t>(1, n) * sizeof(int32_t)));
         p->h_batch_index.assign(n, -1);
@@ -266,12 +272,22 @@ void GPU_HC_Solver::Data_Transfer_From_Host_To_Device() {
         }
         HC_HIP_CHECK(hipMemcpyAsync(p->d_unified_index, h_unified_dHdx_dHdt_Index.data(),
                                     HC_UNIFIED_INDEX_SIZE * sizeof(int32_t), hipMemcpyHostToDevice, p->stream));
+        // triplet edgels + K: abort-mode scoring and the pose recovery of every run
+        if (p->d_edgels && p->edgel_capacity < Num_Of_Triplet_Edgels) {
+            HC_HIP_CHECK(hipFree(p->d_edgels));
+            p->d_edgels = nullptr;
+        }
+        if (!p->d_edgels) {
+            HC_HIP_CHECK(hipMalloc(&p->d_edgels, (size_t)std::max(1, Num_Of_Triplet_Edgels) * 6 * sizeof(float)));
+            p->edgel_capacity = Num_Of_Triplet_Edgels;
+        }
+        if (!p->d_K) HC_HIP_CHECK(hipMalloc(&p->d_K, 9 * sizeof(float)));
+        HC_HIP_CHECK(hipMemcpyAsync(p->d_edgels, h_Triplet_Edge_Locations.data(),
+                                    (size_t)Num_Of_Triplet_Edgels * 6 * sizeof(float), hipMemcpyHostToDevice,
+                                    p->stream));
+        HC_HIP_CHECK(hipMemcpyAsync(p->d_K, h_Camera_Intrinsic_Matrix, 9 * sizeof(float), hipMemcpyHostToDevice,
+                                    p->stream));
         if (Abort_RANSAC_by_Good_Sol) {
-            HC_HIP_CHECK(hipMemcpyAsync(p->d_edgels, h_Triplet_Edge_Locations.data(),
-                                        (size_t)Num_Of_Triplet_Edgels * 6 * sizeof(float), hipMemcpyHostToDevice,
-                                        p->stream));
-            HC_HIP_CHECK(hipMemcpyAsync(p->d_K, h_Camera_Intrinsic_Matrix, 9 * sizeof(float), hipMemcpyHostToDevice,
-                                        p->stream));
             HC_HIP_CHECK(hipMemcpyAsync(p->d_batch_index, p->h_batch_index.data(),
                                         p->h_batch_index.size() * sizeof(int32_t), hipMemcpyHostToDevice, p->stream));
             HC_HIP_CHECK(hipMemsetAsync(p->d_found, 0, 1, p->stream));
@@ -332,6 +348,26 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
     }
     multi_GPUs_time = now_s() - multi_GPUs_time;                                // :446
 
+    // Transform_GPUHC_Sols_to_Trifocal_Relative_Pose + get_Solution_with_Maximal_Support
+    // (:526-527), on the device before the copies back, outside the tracking timer
+    // like the reference's host evaluation
+    const double tp = now_s();
+    for (PerGPU *p : gpus_) {
+        HC_HIP_CHECK(hipSetDevice(p->dev));
+        const hcStatus st = hc_trifocal_pose_support(NT * p->N, p->d_Track, p->d_conv, Num_Of_Triplet_Edgels,
+                                                     p->d_edgels, p->d_K, Pose_Flags, p->d_inliers, p->d_sel,
+                                                     (hcStream)p->stream);
+        if (st != HC_SUCCESS)
+            throw std::runtime_error(std::string("pose support launch failed: status ") + std::to_string((int)st) +
+                                     " (" + hc_last_error_string() + ")");
+        HC_HIP_CHECK(hipMemcpyAsync(&p->h_sel, p->d_sel, sizeof(hcPoseSelection), hipMemcpyDeviceToHost, p->stream));
+    }
+    for (PerGPU *p : gpus_) {
+        HC_HIP_CHECK(hipSetDevice(p->dev));
+        HC_HIP_CHECK(hipStreamSynchronize(p->stream));
+    }
+    pose_time = now_s() - tp;
+
     h_GPU_HC_Track_Sols_Stack.clear();
     h_is_GPU_HC_Sol_Converge_Stack.clear();
     h_is_GPU_HC_Sol_Infinity_Stack.clear();
@@ -387,6 +423,39 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
     Collect_Num_Of_Coverged_Sols.push_back(counts[0]);
     Collect_Num_Of_Real_Sols.push_back(counts[1]);
     Collect_Num_Of_Inf_Sols.push_back(counts[2]);
+    {
+        std::vector<hcPoseSelection> parts;
+        std::vector<int32_t> offs;
+        int off = 0;
+        for (PerGPU *p : gpus_) {
+            parts.push_back(p->h_sel);
+            offs.push_back(off);
+            off += NT * p->N;
+        }
+        hc_pose_merge((int)parts.size(), parts.data(), offs.data(), Pose_Flags, &pose_selection);
+        pose_success = false;
+        for (float &v : pose_residuals) v = -1.0f;
+        if (pose_selection.num_candidates > 0) {                                // :490-503
+            std::cout << "### Found GT pose!" << std::endl;
+            pose_success = hc_pose_residuals(h_Camera_Pose21, h_Camera_Pose31, pose_selection.R21, pose_selection.t21,
+                                             pose_selection.R31, pose_selection.t31, pose_residuals) != 0;
+        }
+        printf("\n## Maximal-support pose (%d candidates, %.3f ms on device):\n", pose_selection.num_candidates,
+               pose_time * 1e3);
+        printf(" - views 1-2: path %d, %d inliers; views 1-3: path %d, %d inliers\n", pose_selection.path21,
+               pose_selection.inliers21, pose_selection.path31, pose_selection.inliers31);
+        std::cout << (pose_success ? "## Found solution matched with GT: " : "## Not found a solution matched with GT: ")
+                  << std::endl;                                                 // :552-565
+        printf(" - Residual of R21: %g (rad)\n - Residual of R31: %g (rad)\n", pose_residuals[0], pose_residuals[1]);
+        printf(" - Residual of t21: %g (m)\n - Residual of t31: %g (m)\n", pose_residuals[2], pose_residuals[3]);
+        PoseRecord rec;
+        rec.success = pose_success ? 1 : 0;
+        for (int k = 0; k < 4; k++) rec.residuals[k] = pose_residuals[k];
+        rec.path21 = pose_selection.path21;
+        rec.path31 = pose_selection.path31;
+        rec.num_candidates = pose_selection.num_candidates;
+        Collect_Pose.push_back(rec);
+    }
     if (Abort_RANSAC_by_Good_Sol) {
         int g = 0;
         for (PerGPU *p : gpus_) {
@@ -418,11 +487,8 @@ void GPU_HC_Solver::Free_Arrays_for_Aborting_RANSAC() {
     if (!Abort_RANSAC_by_Good_Sol) return;
     for (PerGPU *p : gpus_) {
         (void)hipSetDevice(p->dev);
-        (void)hipFree(p->d_edgels);
-        (void)hipFree(p->d_K);
         (void)hipFree(p->d_found);
         (void)hipFree(p->d_batch_index);
-        p->d_edgels = p->d_K = nullptr;
         p->d_found = nullptr;
         p->d_batch_index = nullptr;
     }
@@ -433,7 +499,7 @@ GPU_HC_Solver::~GPU_HC_Solver() {
         (void)hipSetDevice(p->dev);
         void *bufs[] = {p->d_Start_Sols, p->d_Track, p->d_Start_Params, p->d_Target_Params, p->d_diffParams,
                         p->d_unified_index, p->d_conv, p->d_inf, p->d_stats, p->d_ws, p->d_edgels, p->d_K,
-                        p->d_found, p->d_batch_index};
+                        p->d_found, p->d_batch_index, p->d_inliers, p->d_sel};
         for (void *b : bufs)
             if (b) (void)hipFree(b);
         if (p->ev0) (void)hipEventDestroy(p->ev0);
@@ -485,5 +551,17 @@ bool run_GPU_HC_Solver(const HC_Settings &settings, const std::string &root_dir,
     for (size_t i = 0; i < GPU_HC_.Collect_Num_Of_Coverged_Sols.size(); i++)
         sf << GPU_HC_.Collect_Num_Of_Coverged_Sols[i] << "\t" << GPU_HC_.Collect_Num_Of_Real_Sols[i] << "\t"
            << GPU_HC_.Collect_Num_Of_Inf_Sols[i] << "\n";
+    // not in the reference: one line per round -- GT match, residuals (rot21 rot31
+    // transl21 transl31), selected batch ids, number of candidates
+    std::ofstream pf(root + "Output_Write_Files/GPU_Pose_Results.txt");
+    for (size_t i = 0; i < GPU_HC_.Collect_Pose.size(); i++) {
+        const auto &r = GPU_HC_.Collect_Pose[i];
+        pf << r.success << "\t" << r.residuals[0] << "\t" << r.residuals[1] << "\t" << r.residuals[2] << "\t"
+           << r.residuals[3] << "\t" << r.path21 << "\t" << r.path31 << "\t" << r.num_candidates << "\n";
+    }
+    // WRITE_GPUHC_CONVERGED_SOLS (definitions.hpp:22, GPU_HC_Solver.cpp:508-511): last round
+    if (settings.b("Write_Converged_Sols", false))
+        hc_write_converged_sols((root + "Output_Write_Files/GPU_Converged_HC_tracks.txt").c_str(), GPU_HC_.num_samples(),
+                                reinterpret_cast<const float *>(GPU_HC_.tracks().data()), GPU_HC_.converge().data());
     return true;
 }

@@ -4,12 +4,15 @@
 // extraction the reference uses (magmaHC/Data_Reader.cpp), generates the RANSAC
 // target parameters with the host libc srand()/rand() exactly like
 // GPU_HC_Solver::Prepare_Target_Params, and counts solutions like
-// Evaluations::Evaluate_HC_Sols.
+// Evaluations::Evaluate_HC_Sols; merges per-GPU pose selections and measures
+// the relative-pose error against the ground truth like Evaluations.cpp:360-543.
 #include "../../include/hc_host.h"
+#include "../../include/hc_pose.h"
 
 #include <cmath>
 #include <cstdlib>
 #include <fstream>
+#include <iomanip>
 #include <string>
 
 namespace {
@@ -153,6 +156,100 @@ void hc_count_solutions(int N, const float *tracks, const uint8_t *conv, const u
         }
     }
     out[0] = nc; out[1] = nr; out[2] = ni;
+}
+
+int hc_write_converged_sols(const char *file, int N, const float *tracks, const uint8_t *conv) {
+    // Evaluations.cpp:120-143 (same stream manipulators, same layout)
+    std::ofstream f(file);
+    if (!f) return -1;
+    int counter = 0, written = 0;
+    for (int ri = 0; ri < N; ri++) {
+        f << "-------------------- RANSAC Iteration " << ri + 1 << " --------------------\n\n";
+        for (int bs = 0; bs < NT; bs++) {
+            f << std::setprecision(10);
+            const long b = (long)ri * NT + bs;
+            if (conv[b] == 1) {
+                f << counter << "\n";
+                for (int vs = 0; vs < NV; vs++)
+                    f << std::setprecision(20) << tracks[(b * (NV + 1) + vs) * 2] << "\t" << std::setprecision(20)
+                      << tracks[(b * (NV + 1) + vs) * 2 + 1] << "\n";
+                f << "\n";
+                written++;
+            }
+            counter++;
+        }
+        f << "\n";
+    }
+    return written;
+}
+
+void hc_pose_merge(int n, const hcPoseSelection *parts, const int32_t *off, int flags, hcPoseSelection *out) {
+    // one launch over all paths would have max-reduced the same keys (hc_pose.hip)
+    const bool quirks = (flags & HC_POSE_REFERENCE_QUIRKS) != 0;
+    hcPoseSelection r{};
+    r.path21 = r.path31 = -1;
+    r.inliers21 = r.inliers31 = -1;
+    bool have[2] = {false, false};
+    for (int i = 0; i < n; i++) {
+        const hcPoseSelection &p = parts[i];
+        r.num_candidates += p.num_candidates;
+        if (p.num_candidates <= 0) continue;
+        for (int v = 0; v < 2; v++) {
+            const uint64_t k = v == 0 ? p.key21 : p.key31;
+            const uint64_t g = quirks ? k - (uint64_t)(uint32_t)off[i]
+                                      : ((k >> 32) << 32) | (uint64_t)((uint32_t)k + (uint32_t)off[i]);
+            uint64_t &best = v == 0 ? r.key21 : r.key31;
+            if (!have[v] || g > best) {
+                have[v] = true;
+                best = g;
+                if (v == 0) {
+                    r.path21 = p.path21 + off[i]; r.inliers21 = p.inliers21;
+                    for (int j = 0; j < 9; j++) r.R21[j] = p.R21[j];
+                    for (int j = 0; j < 3; j++) r.t21[j] = p.t21[j];
+                } else {
+                    r.path31 = p.path31 + off[i]; r.inliers31 = p.inliers31;
+                    for (int j = 0; j < 9; j++) r.R31[j] = p.R31[j];
+                    for (int j = 0; j < 3; j++) r.t31[j] = p.t31[j];
+                }
+            }
+        }
+    }
+    *out = r;
+}
+
+namespace {
+// Evaluations.cpp:360-374: acos(0.5 * (trace(R_gt' R) - 1.0)), float matrix product / trace
+float rotation_residual(const float *gt, const float *R) {
+    float M[9];
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            float acc = 0.0f;
+            for (int k = 0; k < 3; k++) acc += gt[k * 3 + i] * R[k * 3 + j];   // (R_gt')(i,k) = gt(k,i)
+            M[i * 3 + j] = acc;
+        }
+    float tr = 0.0f;
+    for (int i = 0; i < 3; i++) tr += M[i * 3 + i];
+    return (float)std::acos(0.5 * ((double)tr - 1.0));
+}
+// Evaluations.cpp:376-380 with the GT translation normalised (util.hpp:69-78)
+float translation_residual(const float *gt_t, const float *t) {
+    float g[3] = {gt_t[0], gt_t[1], gt_t[2]};
+    const float n = std::sqrt((g[0] * g[0] + g[1] * g[1]) + g[2] * g[2]);
+    g[0] /= n; g[1] /= n; g[2] /= n;
+    float dot = 0.0f;
+    for (int i = 0; i < 3; i++) dot += g[i] * t[i];
+    return (float)std::fabs((double)dot - 1.0);
+}
+}  // namespace
+
+int hc_pose_residuals(const float *gt21, const float *gt31, const float *R21, const float *t21, const float *R31,
+                      const float *t31, float *out) {
+    // Evaluations.cpp:523-543 (Measure_Relative_Pose_Error)
+    out[0] = rotation_residual(gt21, R21);
+    out[1] = rotation_residual(gt31, R31);
+    out[2] = translation_residual(gt21 + 9, t21);
+    out[3] = translation_residual(gt31 + 9, t31);
+    return ((double)out[2] < 1e-1 && (double)out[3] < 1e-1 && (double)out[0] < 1e-1 && (double)out[1] < 1e-1) ? 1 : 0;
 }
 
 }  // extern "C"

@@ -21,7 +21,7 @@
 
 namespace hc {
 
-static thread_local hipError_t g_last_hip_error = hipSuccess;
+thread_local hipError_t g_last_hip_error = hipSuccess;   // shared with hc_pose.hip (hc_last_error_string)
 static inline hcStatus launch_status(hcStatus on_fail) {
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { g_last_hip_error = e; return on_fail; }

@@ -5,8 +5,9 @@
 //                [-g <num GPUs>] [-t <test rounds>] [--abort]
 //
 // Reads <root>/problems/<problem>/gpuhc_settings.yaml (falls back to
-// <root>/data/problems/...), runs GPU-HC, writes GPU_Timings.txt and
-// GPU_Sols_Statistics.txt under <root>/Output_Write_Files/.  The root defaults
+// <root>/data/problems/...), runs GPU-HC and the device pose recovery, writes
+// GPU_Timings.txt, GPU_Sols_Statistics.txt, GPU_Pose_Results.txt (and with
+// --write-sols GPU_Converged_HC_tracks.txt) under <root>/Output_Write_Files/.  The root defaults
 // to "../../" like the reference binary (run from <repo>/<pkg>/bin).
 #include <cstdio>
 #include <exception>
@@ -25,13 +26,17 @@ static void usage() {
            "  -n, --samples     RANSAC samples per run (NUM_OF_RANSAC_ITERATIONS, default 100)\n"
            "  -g, --gpus        number of GPUs (overrides Num_Of_GPUs)\n"
            "  -t, --times       test rounds (TEST_RANSAC_TIMES, default 1)\n"
-           "      --abort       Abort_RANSAC_by_Good_Sol = true\n");
+           "      --abort       Abort_RANSAC_by_Good_Sol = true\n"
+           "      --write-sols  write Output_Write_Files/GPU_Converged_HC_tracks.txt\n"
+           "      --quirks      reference-literal pose selection (Pose_Selection_Reference_Quirks)\n"
+           "  -s, --dataset     RANSAC dataset directory name (default Synthetic)\n");
 }
 
 int main(int argc, char **argv) {
     std::string problem, root = "../../";
     int samples = -1, gpus = -1, times = 1;
-    bool abort_flag = false;
+    bool abort_flag = false, write_sols = false, quirks = false;
+    std::string dataset;
     if (argc <= 1) { usage(); return 0; }
     for (int i = 1; i < argc; i++) {
         const std::string a = argv[i];
@@ -46,6 +51,9 @@ int main(int argc, char **argv) {
         else if (a == "-g" || a == "--gpus") gpus = std::stoi(next("-g"));
         else if (a == "-t" || a == "--times") times = std::stoi(next("-t"));
         else if (a == "--abort") abort_flag = true;
+        else if (a == "--write-sols") write_sols = true;
+        else if (a == "--quirks") quirks = true;
+        else if (a == "-s" || a == "--dataset") dataset = next("-s");
         else { printf("\033[1;31m[ERROR] Invalid input arguments!\033[0m\n"); usage(); return 0; }
     }
     if (problem.empty()) { usage(); return 0; }
@@ -59,6 +67,9 @@ int main(int argc, char **argv) {
         if (samples > 0) s.set("Num_Of_RANSAC_Iterations", std::to_string(samples));
         if (gpus > 0) s.set("Num_Of_GPUs", std::to_string(gpus));
         if (abort_flag) s.set("Abort_RANSAC_by_Good_Sol", "true");
+        if (write_sols) s.set("Write_Converged_Sols", "true");
+        if (quirks) s.set("Pose_Selection_Reference_Quirks", "true");
+        if (!dataset.empty()) s.set("RANSAC_Dataset", dataset);
         if (!run_GPU_HC_Solver(s, root, times)) return 1;
     } catch (const std::exception &e) {
         std::cerr << "Exception: " << e.what() << std::endl;
