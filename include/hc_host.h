@@ -11,6 +11,8 @@
  *   hc_split_samples          GPU_HC_Solver ctor sample split (GPU_HC_Solver.cpp:85-88)
  *   hc_count_solutions        Evaluations::Evaluate_HC_Sols (magmaHC/Evaluations.cpp:145-182)
  *   hc_write_converged_sols   Evaluations::Write_Converged_Sols (magmaHC/Evaluations.cpp:120-143)
+ *   hc_add_pixel_noise,       noisy synthcurves in the
+ *   hc_write_triplet_edgels   Triplet_Edgels format of Data_Reader.cpp:273-324
  * All complex arrays are interleaved float (re, im) == hcComplex.
  */
 #ifndef HC_HOST_H
@@ -51,6 +53,18 @@ void hc_count_solutions(int num_samples, const float *tracks /* 312N x 31 x 2 */
    Returns the number of paths written, <0 if the file cannot be opened. */
 int hc_write_converged_sols(const char *file, int num_samples, const float *tracks /* 312N x 31 x 2 */,
                             const uint8_t *converge);
+
+/* Noisy synthcurves (not in the reference, which ships noiseless data only):
+   every point of every view is moved by N(0, sigma_px^2) pixel noise and
+   converted back to metric, tangents unchanged.  Pixel u = x*K[0] + K[2],
+   v = y*K[4] + K[5] in double; draws from std::mt19937_64(seed) through
+   std::normal_distribution<double>(0, sigma_px), edgel-major, views 1..3, u
+   then v; x' = (float)((u' - K[2]) / K[0]), y' = (float)((v' - K[5]) / K[4]). */
+void hc_add_pixel_noise(int num_edgels, const float *locations /* E x 6 */, const float *K, double sigma_px,
+                        uint64_t seed, float *noisy_locations /* E x 6 */);
+/* Writes E lines "x1 y1 tx1 ty1 x2 y2 tx2 ty2 x3 y3 tx3 ty3" (%.9g: reads back
+   bit-exactly through hc_read_triplet_edgels).  Returns E, <0 on open failure. */
+int hc_write_triplet_edgels(const char *file, int num_edgels, const float *locations, const float *tangents);
 
 #ifdef __cplusplus
 }

@@ -697,6 +697,73 @@ int orc_pose_residuals(const float *gt21, const float *gt31, const orc_pose_sele
 }
 
 /* ====================================================================== */
+/* Noisy synthcurves.  Restates the C++ standard     */
+/* library pieces the product uses (include/hc_host.h hc_add_pixel_noise):  */
+/* std::mt19937_64 (the standard's parameters), generate_canonical<double, */
+/* 53> over it, and libstdc++'s normal_distribution<double> (Marsaglia     */
+/* polar method, second variate cached).                                   */
+/* ====================================================================== */
+typedef struct { uint64_t mt[312]; int i; } orc_mt64;
+static void mt64_seed(orc_mt64 *g, uint64_t seed) {
+    g->mt[0] = seed;
+    for (int i = 1; i < 312; i++) g->mt[i] = 6364136223846793005ULL * (g->mt[i - 1] ^ (g->mt[i - 1] >> 62)) + (uint64_t)i;
+    g->i = 312;
+}
+static uint64_t mt64_next(orc_mt64 *g) {
+    if (g->i >= 312) {
+        for (int k = 0; k < 312; k++) {
+            const uint64_t y = (g->mt[k] & 0xFFFFFFFF80000000ULL) | (g->mt[(k + 1) % 312] & 0x7FFFFFFFULL);
+            g->mt[k] = g->mt[(k + 156) % 312] ^ (y >> 1) ^ ((y & 1ULL) ? 0xB5026F5AA96619E9ULL : 0ULL);
+        }
+        g->i = 0;
+    }
+    uint64_t z = g->mt[g->i++];
+    z ^= (z >> 29) & 0x5555555555555555ULL;
+    z ^= (z << 17) & 0x71D67FFFEDA60000ULL;
+    z ^= (z << 37) & 0xFFF7EEE000000000ULL;
+    z ^= z >> 43;
+    return z;
+}
+static double canonical53(orc_mt64 *g) {
+    const double r = (double)(mt64_next(g)) / 18446744073709551616.0;   /* one 64-bit draw / 2^64 */
+    return r >= 1.0 ? nextafter(1.0, 0.0) : r;
+}
+typedef struct { orc_mt64 g; int saved_ok; double saved; } orc_normal;
+static double normal_next(orc_normal *n, double sigma) {
+    double ret;
+    if (n->saved_ok) {
+        n->saved_ok = 0;
+        ret = n->saved;
+    } else {
+        double x, y, r2;
+        do {
+            x = 2.0 * canonical53(&n->g) - 1.0;
+            y = 2.0 * canonical53(&n->g) - 1.0;
+            r2 = x * x + y * y;
+        } while (r2 > 1.0 || r2 == 0.0);
+        const double mult = sqrt(-2 * log(r2) / r2);
+        n->saved = x * mult;
+        n->saved_ok = 1;
+        ret = y * mult;
+    }
+    return ret * sigma + 0.0;
+}
+void orc_add_pixel_noise(int E, const float *loc, const float *K, double sigma, uint64_t seed, float *out) {
+    orc_normal n;
+    mt64_seed(&n.g, seed);
+    n.saved_ok = 0;
+    n.saved = 0.0;
+    const double fx = K[0], cx = K[2], fy = K[4], cy = K[5];
+    for (int e = 0; e < E; e++)
+        for (int v = 0; v < 3; v++) {
+            const double u = (double)loc[e * 6 + 2 * v] * fx + cx + normal_next(&n, sigma);
+            const double w = (double)loc[e * 6 + 2 * v + 1] * fy + cy + normal_next(&n, sigma);
+            out[e * 6 + 2 * v] = (float)((u - cx) / fx);
+            out[e * 6 + 2 * v + 1] = (float)((w - cy) / fy);
+        }
+}
+
+/* ====================================================================== */
 /* LAPACK cgesv semantics (call sites CPUHC_Generic_Solver_Eval_by_Indx.cpp:93,100,107,114,127) */
 /* cgetf2 (right-looking, icamax on cabs1, first max) + cgetrs.  The       */
 /* OpenBLAS 0.3.23 kernels the reference links are not reproducible here:  */

@@ -138,6 +138,11 @@ int orc_pose_support(int num_paths, const float *tracks, const uint8_t *conv, in
 int orc_pose_residuals(const float *gt_pose21, const float *gt_pose31, const orc_pose_selection *sel,
                        float *out4);
 
+/* Noisy synthcurves: N(0, sigma_px^2) pixel noise on every point of every view
+   from std::mt19937_64(seed) + libstdc++ normal_distribution<double> (restated). */
+void orc_add_pixel_noise(int num_edgels, const float *loc, const float *K, double sigma_px, uint64_t seed,
+                         float *noisy);
+
 int orc_max_threads(void);
 
 #ifdef __cplusplus

@@ -234,3 +234,10 @@ def pose_residuals(gt21, gt31, sel: dict):
     ok = lib().orc_pose_residuals(_p(np.ascontiguousarray(gt21, np.float32)),
                                   _p(np.ascontiguousarray(gt31, np.float32)), C.byref(s), _p(out))
     return out, bool(ok)
+
+
+def add_pixel_noise(loc, K, sigma_px, seed):
+    out = np.zeros_like(np.ascontiguousarray(loc, np.float32))
+    lib().orc_add_pixel_noise(C.c_int(loc.shape[0]), _p(np.ascontiguousarray(loc, np.float32)),
+                              _p(np.ascontiguousarray(K, np.float32)), C.c_double(sigma_px), C.c_uint64(seed), _p(out))
+    return out

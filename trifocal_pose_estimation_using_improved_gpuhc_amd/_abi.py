@@ -102,6 +102,10 @@ def lib() -> C.CDLL:
         L.hc_pose_merge.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(hcPoseSelection)]
         L.hc_pose_residuals.restype = C.c_int
         L.hc_pose_residuals.argtypes = [C.c_void_p] * 6 + [C.c_void_p]
+        L.hc_add_pixel_noise.restype = None
+        L.hc_add_pixel_noise.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_uint64, C.c_void_p]
+        L.hc_write_triplet_edgels.restype = C.c_int
+        L.hc_write_triplet_edgels.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]
         L.hc_write_converged_sols.restype = C.c_int
         L.hc_write_converged_sols.argtypes = [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]
         L.hc_prepare_target_params.argtypes = [C.c_uint, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
@@ -128,4 +132,5 @@ DECLARED_SYMBOLS = (
     "hc_count_triplet_edgels", "hc_read_triplet_edgels", "hc_split_samples", "hc_prepare_target_params",
     "hc_count_solutions",
     "hc_trifocal_pose_support", "hc_pose_merge", "hc_pose_residuals", "hc_write_converged_sols",
+    "hc_add_pixel_noise", "hc_write_triplet_edgels",
 )

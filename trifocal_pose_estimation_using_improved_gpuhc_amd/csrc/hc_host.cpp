@@ -10,7 +10,9 @@
 #include "../../include/hc_pose.h"
 
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
+#include <random>
 #include <fstream>
 #include <iomanip>
 #include <string>
@@ -181,6 +183,31 @@ int hc_write_converged_sols(const char *file, int N, const float *tracks, const 
         f << "\n";
     }
     return written;
+}
+
+void hc_add_pixel_noise(int E, const float *loc, const float *K, double sigma, uint64_t seed, float *out) {
+    std::mt19937_64 gen(seed);
+    std::normal_distribution<double> noise(0.0, sigma);
+    const double fx = K[0], cx = K[2], fy = K[4], cy = K[5];
+    for (int e = 0; e < E; e++)
+        for (int v = 0; v < 3; v++) {
+            const double u = (double)loc[e * 6 + 2 * v] * fx + cx + noise(gen);
+            const double w = (double)loc[e * 6 + 2 * v + 1] * fy + cy + noise(gen);
+            out[e * 6 + 2 * v] = (float)((u - cx) / fx);
+            out[e * 6 + 2 * v + 1] = (float)((w - cy) / fy);
+        }
+}
+
+int hc_write_triplet_edgels(const char *file, int E, const float *loc, const float *tan) {
+    FILE *f = std::fopen(file, "w");
+    if (!f) return -1;
+    for (int e = 0; e < E; e++) {
+        for (int v = 0; v < 3; v++)
+            std::fprintf(f, "%.9g %.9g %.9g %.9g%s", loc[e * 6 + 2 * v], loc[e * 6 + 2 * v + 1], tan[e * 6 + 2 * v],
+                         tan[e * 6 + 2 * v + 1], v < 2 ? " " : "\n");
+    }
+    std::fclose(f);
+    return E;
 }
 
 void hc_pose_merge(int n, const hcPoseSelection *parts, const int32_t *off, int flags, hcPoseSelection *out) {
