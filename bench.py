@@ -9,7 +9,14 @@ tracking launch over the rank's samples, inputs already resident in HBM.
 
 Multi-GPU: one process per GPU (torch.distributed, backend nccl == RCCL);
 samples are independent so the ranks share nothing on the data path (weak
-scaling); RCCL only carries the barrier and the max-over-ranks timing.
+scaling); RCCL only carries the barrier, the max-over-ranks timing, the
+early-stop flag (abort leg) and the 136-byte pose selections (all_gather).
+
+Besides the headline line (config 2) the JSON carries: `pose` (device pose
+recovery + maximal support over the config-2 tracks),
+`early_abort` (config 3 / 4: time-to-first-good-pose), `noisy_pose` (config 5:
+sigma=1px noisy synthcurves, pose success rate vs paths/s), `roofline` and
+`cpu_baseline`.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--samples S] [--no-cpu-baseline]
 """
@@ -47,6 +54,9 @@ def parse():
                     help="samples per GPU of the early-abort (config 3/4) time-to-first-good-pose run; 0 disables")
     ap.add_argument("--abort-chunk", type=int, default=125,
                     help="samples per launch in the early-abort run (the cross-GPU flag is reduced between launches)")
+    ap.add_argument("--noisy-trials", type=int, default=10,
+                    help="config 5: RANSAC runs on sigma=1px noisy synthcurves (pose success rate); 0 disables")
+    ap.add_argument("--noisy-sigma", type=float, default=1.0)
     return ap.parse_args()
 
 
@@ -106,6 +116,22 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+
+    # device pose recovery + maximal support over the launch's tracks,
+    # timed separately with HIP events on the same stream
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import pose as P
+    tr.set_ransac_data(data)
+    inl = torch.empty((S * 312, 2), dtype=torch.int32, device=dev)
+    sel = torch.empty(P.SEL_BYTES, dtype=torch.uint8, device=dev)
+    pev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a_, b_ in pev:
+        a_.record(stream)
+        P.launch_pose_support(res.tracks, res.converge, tr.edgels, tr.K, inl, sel, stream=stream)
+        b_.record(stream)
+    torch.cuda.synchronize(dev)
+    pose_ms = float(np.median([a_.elapsed_time(b_) for a_, b_ in pev]))
+    merged = sharding_gather(sel, rank * S * 312)
+    pose_res, pose_ok = P.residuals(data, merged)
 
     host = res.host()
     steps_sum = int(host["stats"]["steps"].astype(np.int64).sum())
@@ -174,6 +200,10 @@ def main():
                       "note": "device clock (s_memrealtime) from the first chunk's start, min over ranks; "
                               "wall = host time to the all-GPU sync, max over ranks"}
 
+    noisy_info = None
+    if args.noisy_trials > 0:
+        noisy_info = noisy_pose_leg(args, tr, problem, data, world, rank, dev, stream)
+
     if rank == 0:
         med_launch_s = float(np.median(launch_ms)) / 1e3
         achieved_tf = flops / med_launch_s / 1e12
@@ -211,7 +241,16 @@ def main():
                          "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
                          "rk4_steps": steps_sum, "corrections": corr_sum},
             "solutions": {"converged": counts[0], "real": counts[1], "infinity": counts[2]},
+            "pose": {"pose_support_ms": round(pose_ms, 4), "candidates": merged["num_candidates"],
+                     "path21": merged["path21"], "path31": merged["path31"], "inliers21": merged["inliers21"],
+                     "inliers31": merged["inliers31"], "gt_match": pose_ok,
+                     "residuals": [round(float(v), 6) for v in pose_res],
+                     "note": "device candidate filter + Cayley pose + reprojection inlier scoring of every "
+                             "candidate over all triplet edgels + maximal-support selection "
+                             "(Evaluations.cpp:298-504), merged over ranks (RCCL all_gather)"},
         }
+        if noisy_info is not None:
+            line["noisy_pose"] = noisy_info
         if abort_info is not None:
             line["early_abort"] = abort_info
         if not args.no_cpu_baseline:
@@ -219,6 +258,64 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def sharding_gather(sel, path_offset):
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import sharding
+    return sharding.gather_pose_selection(sel, path_offset)
+
+
+def noisy_pose_leg(args, tr, problem, data, world, rank, dev, stream):
+    """BASELINE.json config 5 (path pruning is always on in the tracker): RANSAC
+    runs of samples_per_gpu*world samples on sigma-px noisy synthcurves, one
+    noise seed per trial; each run = track + device pose support, selection
+    merged over ranks; success = the selected pose matches GT within the
+    reference's 0.1 rad / 0.1 tolerances (Evaluations.cpp:523-543)."""
+    import torch
+    import torch.distributed as dist
+
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import pose as P
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import prepare_target_params, sharding, synthcurves
+    S = args.samples
+    res = tr.allocate(S, stats=False)
+    inl = torch.empty((S * 312, 2), dtype=torch.int32, device=dev)
+    sel = torch.empty(P.SEL_BYTES, dtype=torch.uint8, device=dev)
+    ok_list, times, cands = [], [], []
+    for t in range(args.noisy_trials):
+        nd = synthcurves.noisy(data, args.noisy_sigma, synthcurves.DEFAULT_SEED + t)
+        ta, da, _ = prepare_target_params(problem, nd, seed=t, num_samples=S * world, num_gpus=world)
+        off, cnt = sharding.shard(S * world, world, rank)
+        tg = torch.from_numpy(ta[off:off + cnt]).to(dev)
+        df = torch.from_numpy(da[off:off + cnt]).to(dev)
+        tr.set_ransac_data(nd)
+        tr.reset_tracks(res)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        tr.launch(tg, df, res, stream=stream)
+        P.launch_pose_support(res.tracks, res.converge, tr.edgels, tr.K, inl, sel, stream=stream)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        times.append(time.perf_counter() - t0)
+        m = sharding.gather_pose_selection(sel, off * 312)
+        ok_list.append(P.residuals(nd, m)[1])
+        cands.append(m["num_candidates"])
+    tt = float(np.sum(times))
+    if world > 1:
+        v = torch.tensor([tt], dtype=torch.float64, device=dev)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        tt = float(v.item())
+    tr.set_ransac_data(data)
+    return {"workload": "config 5: path pruning (depth-sign truncation, always on) + sigma=%g px noisy "
+                        "synthcurves (Triplet_Edgels_000, noise seed 20250215+trial), track + device pose "
+                        "support per RANSAC run" % args.noisy_sigma,
+            "sigma_px": args.noisy_sigma, "trials": args.noisy_trials, "samples_per_run": S * world,
+            "success_rate": round(float(np.mean(ok_list)), 4),
+            "paths_per_s": round(312 * S * world * args.noisy_trials / tt, 1),
+            "ms_per_run": round(tt / args.noisy_trials * 1e3, 3),
+            "median_candidates": int(np.median(cands))}
 
 
 def traffic_bytes(version):

@@ -99,3 +99,53 @@ def test_pass_in_first_chunk_of_rank0(tmp_path):
     res = _run(2, 41, 8, [3], tmp_path)            # uneven shards: 21 / 20
     assert [r[0] for r in res] == [3, 3]
     assert [r[2:] for r in res] == [[0], [0]]
+
+
+def _pose_worker(rank, world, port, cuts, out_dir):
+    """Each rank selects over its shard with the oracle (standing in for the
+    device kernel) and the shards are merged through gather_pose_selection."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle import oracle as O
+        from test_pose import _fixture_tracks
+        from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi, load_ransac_data
+        d = load_ransac_data(0)
+        g, tr, conv = _fixture_tracks()
+        tr[312 * 99 + 7] = tr[int(g["path"][0])]
+        conv[312 * 99 + 7] = 1
+        a, b = cuts[rank] * 312, cuts[rank + 1] * 312
+        _, s = O.pose_support(tr[a:b], conv[a:b], d.locations, d.K)
+        st = _abi.hcPoseSelection()
+        for k in ("num_candidates", "path21", "inliers21", "path31", "inliers31"):
+            setattr(st, k, int(s[k]))
+        if s["num_candidates"]:
+            st.key21 = (s["inliers21"] << 32) | s["path21"]
+            st.key31 = (s["inliers31"] << 32) | s["path31"]
+        for k in ("R21", "t21", "R31", "t31"):
+            getattr(st, k)[:] = [float(v) for v in s[k]]
+        raw = torch.from_numpy(np.frombuffer(bytes(st), np.uint8).copy())
+        m = sharding.gather_pose_selection(raw, a)
+        np.save(os.path.join(out_dir, f"p{rank}.npy"),
+                np.array([m["num_candidates"], m["path21"], m["inliers21"], m["path31"], m["inliers31"]], np.int64))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pose_selection_merges_across_ranks(tmp_path, oracle):
+    """world 2 (gloo): merged selection == the oracle's selection over all paths."""
+    from test_pose import _fixture_tracks
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import load_ransac_data
+    d = load_ransac_data(0)
+    g, tr, conv = _fixture_tracks()
+    tr[312 * 99 + 7] = tr[int(g["path"][0])]
+    conv[312 * 99 + 7] = 1
+    full = oracle.pose_support(tr, conv, d.locations, d.K)[1]
+    cuts = [0, 68, 100]
+    mp.start_processes(_pose_worker, args=(2, _free_port(), cuts, str(tmp_path)), nprocs=2, join=True,
+                       start_method="fork")
+    exp = [full["num_candidates"], full["path21"], full["inliers21"], full["path31"], full["inliers31"]]
+    for r in range(2):
+        assert np.load(os.path.join(tmp_path, f"p{r}.npy")).tolist() == exp

@@ -11,6 +11,10 @@ data path needs no collective.  RCCL carries only:
     the reduced flag into the workspace, so every rank skips its remaining
     paths once any rank has found a passing hypothesis.  Nothing synchronises
     with the host between chunks (stream order does it);
+  * the maximal-support pose: each rank selects over its own paths on the
+    device (hc_trifocal_pose_support); the 136-byte selections are
+    all-gathered and merged by key (hc_pose_merge) as if one launch had
+    covered every rank's paths (gather_pose_selection);
   * timing (barrier, max / min over ranks) in bench.py.
 
 The reference has no cross-GPU early stop: each GPU keeps its own flag
@@ -80,3 +84,25 @@ def global_batch_ids(local_batch_index: np.ndarray, chunk_offset: int, shard_off
     ids = np.asarray(local_batch_index)
     ids = ids[ids >= 0]
     return ids + 312 * (chunk_offset + shard_offset)
+
+
+def gather_pose_selection(selection, path_offset: int, group=None, quirks: bool = False) -> dict:
+    """All-gathers every rank's raw hcPoseSelection bytes (a uint8 tensor on the
+    rank's device, or on the CPU for gloo) and merges them with the ranks'
+    first global batch ids.  Returns the merged selection (global batch ids)
+    on every rank."""
+    import torch
+    import torch.distributed as dist
+
+    from . import pose
+    multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    if not multi:
+        return pose.merge([selection], [path_offset], quirks)
+    world = dist.get_world_size(group)
+    sel = selection.reshape(-1)[:pose.SEL_BYTES].contiguous()
+    parts = [torch.empty_like(sel) for _ in range(world)]
+    dist.all_gather(parts, sel, group=group)
+    off = torch.tensor([path_offset], dtype=torch.int64, device=sel.device)
+    offs = [torch.empty_like(off) for _ in range(world)]
+    dist.all_gather(offs, off, group=group)
+    return pose.merge([p.cpu().numpy() for p in parts], [int(o.item()) for o in offs], quirks)
