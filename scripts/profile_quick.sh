@@ -1,0 +1,13 @@
+# usage: bash scripts/profile_quick.sh TAG  -- kernel trace + 2 PMC passes (VALU/LDS issue, LDS banks) of a short bench run
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+T=$1
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline --abort-samples 0 --noisy-trials 0"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_trace -o run -- $B > gpurun_out/${T}_trace.log 2>&1; rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
+i=0
+for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY" \
+           "SQ_INSTS_SALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS SQ_IFETCH"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $set --output-format csv -d gpurun_out/${T}_pmc$i -o run -- $B > gpurun_out/${T}_pmc$i.log 2>&1; rc=$?; echo "pmc$i rc=$rc"; [ $rc -eq 0 ] || exit $rc
+done
+python scripts/pmc_summary.py $T gpurun_out/${T}_pmc_summary.json "$HC_TRIFOCAL_KERNEL" > /dev/null

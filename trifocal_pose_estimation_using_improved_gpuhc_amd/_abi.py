@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libhc_trifocal.so")
+# HC_TRIFOCAL_LIB: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("HC_TRIFOCAL_LIB") or os.path.join(PKG_DIR, "lib", "libhc_trifocal.so")
 
 NUM_VARS, NUM_PARAMS, NUM_TRACKS = 30, 33, 312
 NPP = NUM_PARAMS + 1

@@ -13,6 +13,8 @@
 // with all 64 lanes and raises an agent-scope flag.
 #include "hc_device.hpp"
 #include "hc_lu3.hpp"
+#include "hc_track4.hpp"
+#include "hc_lu3s.hpp"
 #include "../../include/hc_trifocal.h"
 
 #include <atomic>
@@ -28,11 +30,25 @@ static inline hcStatus launch_status(hcStatus on_fail) {
     return HC_SUCCESS;
 }
 
+// Longest-processing-time-first dequeue order (scripts/make_track_order.py):
+// queue position q -> track c_track_order[q / N], sample q % N.  Results are
+// per batch id, so the order only changes when a path runs, not what it computes.
+__constant__ int c_track_order[NTRK] = {
+#include "hc_track_order.inc"
+};
+__device__ __forceinline__ int path_of_queue_pos(int q, int num_paths, int ordered) {
+    if (!ordered) return q;
+    const int n = num_paths / NTRK;          // samples in this launch
+    const int rank = q / n;
+    return (q - rank * n) * NTRK + c_track_order[rank];
+}
+
 constexpr int WG_THREADS = 256;
 constexpr int WAVES_PER_WG = WG_THREADS / WAVE;
 
 struct KArgs {
     int num_paths;
+    int ordered;        // dequeue track-major in c_track_order (abort mode off)
     int max_steps, max_corr, inc_steps;
     const cf *start_sols;
     const cf *const *start_sols_array;
@@ -444,8 +460,10 @@ __device__ __forceinline__ int half_sum_i(int v) {
 
 template <bool ABORT, int MINW, int V>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
-    // V = 2: bpermute LU + v2 evals; V = 3: LDS-broadcast LU + packed v3 evals
-    constexpr int TAB_BYTES = V == 3 ? (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32)
+    // V = 2: bpermute LU + v2 evals; V = 3: LDS-broadcast LU + packed v3 evals;
+    // V = 8: v3 evals + the structurally sparse LU of hc_lu3s.hpp
+    constexpr bool EV3 = V >= 3;
+    constexpr int TAB_BYTES = EV3 ? (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32)
                                      : (int)(sizeof(uint32_t) * (HX2_SLOT_CAP + HT_TERMS) * 32);
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
@@ -453,13 +471,13 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     TableWS *ws = a.ws;
     TableWS2 *w2 = a.ws2;
     TableWS3 *w3 = a.ws3;
-    if ((ws->status | (unsigned)w2->status | (V == 3 ? (unsigned)w3->status : 0u)) != 0u) return;
-    const int hx_len = V == 3 ? w3->hx_len : w2->hx_len;
+    if ((ws->status | (unsigned)w2->status | (EV3 ? (unsigned)w3->status : 0u)) != 0u) return;
+    const int hx_len = EV3 ? w3->hx_len : w2->hx_len;
     uint32_t *s_hx2 = reinterpret_cast<uint32_t *>(s_tab);
     uint32_t *s_ht = s_hx2 + HX2_SLOT_CAP * 32;
     uint2 *s_hx3 = reinterpret_cast<uint2 *>(s_tab);
     uint2 *s_ht3 = s_hx3 + HX3_SLOT_CAP * 32;
-    if constexpr (V == 3) {
+    if constexpr (EV3) {
         for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];
         for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = w3->ht[i];
     } else {
@@ -480,6 +498,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     if (r == 30) S.x[30] = cmk(1.0f, 0.0f);
     if (r == 0) S.p[33] = cmk(1.0f, 0.0f);
     const uint32_t map[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
+    const uint32_t row_pat = V == 8 ? row_pattern(map) : 0u;   // structural pattern of row r (v8 LU)
     const bool rl = r < NV;
     wave_lds_sync();
 
@@ -556,7 +575,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
                     ph = PH_IDLE;
                     b = -1;
                 } else {
-                    b = nb;
+                    b = path_of_queue_pos(nb, a.num_paths, a.ordered);
                     bool skip = false;
                     if (ABORT) {                                              // TrunRANSAC.cu:152
                         skip = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
@@ -654,20 +673,21 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
         const bool act = ph_in == PH_STAGE;
         const bool pred = act && s_in < 4;
         cf rA[NV];
-        if constexpr (V == 3) eval_hx3(rA, s_hx3, hx_len, map, S, r_v);     // :184 / :220
+        if constexpr (EV3) eval_hx3(rA, s_hx3, hx_len, map, S, r_v);     // :184 / :220
         else eval_hx2(rA, s_hx2, hx_len, map, S, r_v);
         cf rB = cmk(0.0f, 0.0f);
         if (__ballot(pred) != 0ull) {                                        // :185
-            const cf t = V == 3 ? eval_ht3(s_ht3, S, r_v) : eval_ht2(s_ht, S, r_v);
+            const cf t = EV3 ? eval_ht3(s_ht3, S, r_v) : eval_ht2(s_ht, S, r_v);
             if (pred) rB = t;
         }
         if (__ballot(act && !pred) != 0ull) {                                // :221
-            const cf t = V == 3 ? eval_h3(s_ht3, S, r_v) : eval_h2(s_ht, S, r_v);
+            const cf t = EV3 ? eval_h3(s_ht3, S, r_v) : eval_h2(s_ht, S, r_v);
             if (!pred) rB = t;
         }
         wave_lds_sync();
         cf k;                                                                // :188 / :224
-        if constexpr (V == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
+        if constexpr (V == 8) k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));
+        else if constexpr (V == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
         else k = lu_solve2(rA, rB, lane_v);
         wave_lds_sync();
         {
@@ -723,6 +743,281 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
                         succ++;
                         xl = x;
                         sols = x;
+                        if (succ >= a.inc_steps) { succ = 0; dt *= 2.0f; }
+                    }
+                    stepidx++;
+                    ph = PH_BEGIN;
+                }
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------- tracker v4
+// Four paths per wavefront (hc_track4.hpp): each 16-lane DPP row is a path
+// slot with its own stage machine (t, step size, stage, path id uniform per
+// row); lane r owns rows / unknowns r and r + 16.  One loop iteration runs one
+// predictor or corrector stage (p(t), dH/dx, dH/dt|H, LU) for all four slots.
+// The stage logic is k_track2's (..._TrunPaths.cu:138-280) per row.
+template <bool ABORT>
+__global__ void __launch_bounds__(WG_THREADS, 2) k_track4(KArgs a) {
+    constexpr int TAB_BYTES = (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32);
+    __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
+    __shared__ cf s_sp[NPP];
+    __shared__ SlotLDS4 s_slot[4 * WAVES_PER_WG];
+    TableWS *ws = a.ws;
+    TableWS2 *w2 = a.ws2;
+    TableWS3 *w3 = a.ws3;
+    if ((ws->status | (unsigned)w2->status | (unsigned)w3->status) != 0u) return;
+    const int hx_len = w3->hx_len;
+    uint2 *s_hx3 = reinterpret_cast<uint2 *>(s_tab);
+    uint2 *s_ht3 = s_hx3 + HX3_SLOT_CAP * 32;
+    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = rebase_p_offsets(w3->hx[i]);
+    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = rebase_p_offsets(w3->ht[i]);
+    if (threadIdx.x < NPP) s_sp[threadIdx.x] = a.start_params[threadIdx.x];
+    {
+        float *z = reinterpret_cast<float *>(s_slot);
+        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
+    }
+    __syncthreads();
+    if (ABORT && threadIdx.x == 0) atomicCAS(&ws->t_start, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    const int lane = lane_id();
+    const int r = lane & 15, qb = lane & 48;
+    const int wid = threadIdx.x / WAVE;
+    SlotLDS4 &S = s_slot[wid * 4 + (qb >> 4)];
+    if (r == 0) { S.x[30] = cmk(1.0f, 0.0f); S.p[33] = cmk(1.0f, 0.0f); }
+    const uint32_t map0[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
+    const uint32_t map1[3] = {w2->map[0][r + QL], w2->map[1][r + QL], w2->map[2][r + QL]};
+    const bool v1 = r + QL < NV;   // slot 1 holds a real row / unknown
+    wave_lds_sync();
+
+    int ph = PH_DEQ, b = -1, smp_loaded = -1;
+    int s = 0, stepidx = 0, coef = 1, succ = 0, nsteps = 0, ncorr = 0;
+    float t0 = 0.0f, t_step = 0.0f, dt = 0.01f, h2 = 0.0f, scale = 0.0f;
+    bool end_zone = false, check = true, isSucc = false, isInf = false;
+    const cf z0 = cmk(0.0f, 0.0f);
+    cf x0 = z0, x1 = z0, xl0 = z0, xl1 = z0, so0 = z0, so1 = z0;
+    cf tg0 = z0, tg1 = z0, tg2 = z0;   // target params r, r + 16, 32 of the slot's sample
+
+    for (;;) {
+        for (;;) {
+            if (ph == PH_FINISH) {                                            // :282-286
+                const bool conv = ((double)t0 >= 1.0 || (1.0 - (double)t0 <= 0.0000001));
+                cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+                dtrack[r] = x0;
+                if (v1) dtrack[r + QL] = x1;
+                int in21 = 0, in31 = 0;
+                if (ABORT && conv) {                                          // TrunRANSAC.cu:312-322
+                    S.x[r] = x0;
+                    if (v1) S.x[r + QL] = x1;
+                    wave_lds_sync();
+                    const unsigned long long im =
+                        __ballot(v1 && r >= 2 && (double)__builtin_fabsf(x1.y) < 1e-5);   // x[18..29]
+                    if (((unsigned)(im >> qb) & 0x3FFCu) == 0x3FFCu) {       // eval.cuh:46-53
+                        Hyp hy;
+                        make_hypothesis(S.x, hy);
+                        const float fx = a.K[0], fy = a.K[4], cx = a.K[3] /* eval quirk */, cy = a.K[5];
+                        const float *R = hy.R;
+                        const float d18 = hy.T[0], d19 = hy.T[1], d20 = hy.T[2], d21 = hy.T[3], d22 = hy.T[4], d23 = hy.T[5];
+                        int c21 = 0, c31 = 0;
+                        for (int e = r; e < a.num_edgels; e += QL) {
+                            const float *g = a.edgels + (size_t)e * 6;
+                            const float g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4], g5 = g[5];
+                            float num, den, w0v, w1v, w2v, ex, ey;
+                            num = d20 * (R[2] * g2 + R[5] * g3 + R[8]) - (R[2] * d18 + R[5] * d19 + R[8] * d20);
+                            den = 1.0f - (R[6] * g0 + R[7] * g1 + R[8]) * (R[2] * g2 + R[5] * g3 + R[8]);
+                            w2v = num * (R[6] * g0 + R[7] * g1 + R[8]) + den * d20;
+                            w0v = (num * (R[0] * g0 + R[1] * g1 + R[2]) + den * d18) / w2v;
+                            w1v = (num * (R[3] * g0 + R[4] * g1 + R[5]) + den * d19) / w2v;
+                            ex = (w0v * fx + cx) - (g2 * fx + cx);
+                            ey = (w1v * fy + cy) - (g3 * fy + cy);
+                            c21 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+                            num = d23 * (R[11] * g4 + R[14] * g5 + R[17]) - (R[11] * d21 + R[14] * d22 + R[17] * d23);
+                            den = 1.0f - (R[15] * g0 + R[16] * g1 + R[17]) * (R[11] * g4 + R[14] * g5 + R[17]);
+                            w2v = num * (R[15] * g0 + R[16] * g1 + R[17]) + den * d23;
+                            w0v = (num * (R[9] * g0 + R[10] * g1 + R[11]) + den * d21) / w2v;
+                            w1v = (num * (R[12] * g0 + R[13] * g1 + R[14]) + den * d22) / w2v;
+                            ex = (w0v * fx + cx) - (g4 * fx + cx);
+                            ey = (w1v * fy + cy) - (g5 * fy + cy);
+                            c31 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+                        }
+                        in21 = row_sum_i(c21);
+                        in31 = row_sum_i(c31);
+                        const float r21 = (float)in21 / (float)a.num_edgels, r31 = (float)in31 / (float)a.num_edgels;
+                        if ((double)r21 >= 0.90 && (double)r31 >= 0.90 && r == 0) {   // eval.cuh:241-246
+                            __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            a.found_flag[0] = 1;
+                            a.batch_index[b] = b;
+                            atomicCAS(&ws->t_found, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+                        }
+                    }
+                }
+                if (r == 0) {
+                    a.conv[b] = conv ? 1 : 0;
+                    a.inf[b] = isInf ? 1 : 0;
+                    if (a.stats) a.stats[b] = hcPathStats{nsteps, ncorr, in21, in31};
+                }
+                ph = PH_DEQ;
+            }
+            if (ph == PH_DEQ) {
+                int nb = 0;
+                if (r == 0) nb = (int)atomicAdd(&ws->queue, 1u);
+                nb = qbcast0_i(nb);
+                if (nb >= a.num_paths) {
+                    ph = PH_IDLE;
+                    b = -1;
+                } else {
+                    b = path_of_queue_pos(nb, a.num_paths, a.ordered);
+                    bool skip = false;
+                    if (ABORT) {                                              // TrunRANSAC.cu:152
+                        int f = 0;
+                        if (r == 0) f = (int)__hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        skip = qbcast0_i(f) != 0;
+                        if (skip && r == 0) {
+                            a.conv[b] = 0;
+                            a.inf[b] = 0;
+                            if (a.stats) a.stats[b] = hcPathStats{0, 0, 0, 0};
+                        }
+                    }
+                    if (!skip) {
+                        const int trk = b % NTRK, smp = b / NTRK;            // :67-69
+                        if (smp != smp_loaded) {
+                            const cf *tp = a.target_params + (size_t)smp * NPP;
+                            const cf *dp = a.diff_params + (size_t)smp * NPP;
+                            tg0 = tp[r]; tg1 = tp[r + QL]; tg2 = tp[2 * QL];
+                            S.dif[r] = dp[r];
+                            S.dif[r + QL] = dp[r + QL];
+                            if (r < NPP - 2 * QL) S.dif[r + 2 * QL] = dp[r + 2 * QL];
+                        }
+                        smp_loaded = smp;
+                        const cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+                        const cf *dstart = a.start_sols_array ? a.start_sols_array[trk]
+                                                              : a.start_sols + (size_t)trk * (NV + 1);
+                        x0 = dtrack[r];                                       // :101-103
+                        x1 = v1 ? dtrack[r + QL] : z0;
+                        so0 = dstart[r];
+                        so1 = v1 ? dstart[r + QL] : z0;
+                        xl0 = x0; xl1 = x1;
+                        t0 = 0.0f; t_step = 0.0f; dt = 0.01f;                 // :80
+                        end_zone = false; check = true; isSucc = false; isInf = false;
+                        succ = 0; nsteps = 0; ncorr = 0; stepidx = 0;
+                        ph = PH_BEGIN;
+                    }
+                }
+            }
+            if (ph == PH_BEGIN) {                                             // :138-165
+                bool done = stepidx > a.max_steps;
+                if (!done) done = !((double)t0 < 1.0 && (1.0 - (double)t0 > 0.0000001));
+                if (!done) {
+                    if (!end_zone && (double)__builtin_fabsf(1.0f - t0) <= 0.0500001) end_zone = true;
+                    if (check) {
+                        const unsigned long long pos = __ballot(r < 8 && x0.x > 0.0f);
+                        const bool allpos = ((unsigned)(pos >> qb) & 0xFFu) == 0xFFu;
+                        if (t0 > 0.0f) check = !allpos;
+                    }
+                    done = (double)t0 > 0.95 && check;
+                }
+                if (!done) {
+                    if (end_zone) {
+                        if (dt > __builtin_fabsf(1.0f - t0)) dt = __builtin_fabsf(1.0f - t0);
+                    } else if ((double)dt > __builtin_fabs(0.95 - (double)t0)) {
+                        dt = (float)__builtin_fabs(0.95 - (double)t0);
+                    }
+                    t_step = t0;
+                    h2 = (float)(0.5 * (double)dt);
+                    scale = 0.0f;
+                    coef = 1;
+                    s = 0;
+                    nsteps++;
+                }
+                ph = done ? PH_FINISH : PH_STAGE;
+            }
+            if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
+        }
+        if (__ballot(ph == PH_STAGE) == 0ull) break;
+
+        // ---------------- one stage for all four slots
+        S.x[r] = x0;
+        if (v1) S.x[r + QL] = x1;
+        const bool act = ph == PH_STAGE;
+        const bool pred = act && s < 4;
+        if (pred) {                                                           // :181 p(t), i < 33
+            const float omt = (float)(1.0 - (double)t0);
+            S.p[r] = cadd(cscale(tg0, t0), cscale(s_sp[r], omt));
+            S.p[r + QL] = cadd(cscale(tg1, t0), cscale(s_sp[r + QL], omt));
+            if (r == 0) S.p[32] = cadd(cscale(tg2, t0), cscale(s_sp[32], omt));
+        }
+        wave_lds_sync();
+        // opaque lane id: keeps LICM from hoisting lane-derived per-pivot constants
+        int lane_v = lane;
+        asm volatile("" : "+v"(lane_v));
+        const int r_v = lane_v & 15;
+        cf A0[NV], A1[NV];
+        eval_hx4(A0, A1, s_hx3, hx_len, map0, map1, S, r_v);                 // :184 / :220
+        cf b0 = z0, b1 = z0;
+        if (__ballot(pred) != 0ull) {                                         // :185
+            cf t0v, t1v;
+            eval_ht4(s_ht3, S, r_v, t0v, t1v);
+            if (pred) { b0 = t0v; b1 = t1v; }
+        }
+        if (__ballot(act && !pred) != 0ull) {                                 // :221
+            cf t0v, t1v;
+            eval_h4(s_ht3, S, r_v, t0v, t1v);
+            if (!pred) { b0 = t0v; b1 = t1v; }
+        }
+        wave_lds_sync();
+        cf k0, k1;                                                            // :188 / :224
+        lu_solve4(A0, A1, b0, b1, lane_v, *reinterpret_cast<LUBuf *>(S.ent), k0, k1);
+        wave_lds_sync();
+        if (act) {
+            bool step_end = false;
+            if (pred) {
+                if (s < 3) {                                                  // :191-205
+                    const float w = (float)((double)coef * 1.0 / 6.0);
+                    so0 = cadd(so0, cscale(cscale(k0, dt), w));
+                    so1 = cadd(so1, cscale(cscale(k1, dt), w));
+                    if (coef > 1) { x0 = xl0; x1 = xl1; }
+                    const int sc = (s == 1) ? 0 : 1;
+                    scale += (float)sc * h2;
+                    coef <<= sc;
+                    x0 = cadd(x0, cscale(k0, scale));
+                    x1 = cadd(x1, cscale(k1, scale));
+                    t0 += (float)sc * h2;
+                } else {                                                      // :209-210
+                    so0 = cadd(so0, cdivs(cscale(cscale(k0, dt), 1.0f), 6.0f));
+                    so1 = cadd(so1, cdivs(cscale(cscale(k1, dt), 1.0f), 6.0f));
+                    x0 = so0;
+                    x1 = so1;
+                }
+                if (!v1) { x1 = z0; so1 = z0; }
+                s++;
+                if (s == 4 && a.max_corr <= 0) step_end = true;
+            } else {                                                          // :228-249
+                x0 = csub(x0, k0);
+                x1 = v1 ? csub(x1, k1) : z0;
+                ncorr++;
+                const float vs = (k0.x * k0.x + k0.y * k0.y) + (v1 ? k1.x * k1.x + k1.y * k1.y : 0.0f);
+                const float vc = (x0.x * x0.x + x0.y * x0.y) + (v1 ? x1.x * x1.x + x1.y * x1.y : 0.0f);
+                const float ns = tree_sum_q(vs), nc = tree_sum_q(vc);
+                isSucc = (double)ns < 0.000001 * (double)nc;
+                isInf = (double)nc > 1e14;
+                if (isInf || isSucc || (s - 4) + 1 >= a.max_corr) step_end = true;
+                else s++;
+            }
+            if (step_end) {
+                if (isInf) {                                                  // :252
+                    ph = PH_FINISH;
+                } else {
+                    if (!isSucc) {                                            // :257-265
+                        dt = (float)((double)dt * 0.5);
+                        x0 = xl0; x1 = xl1;
+                        so0 = xl0; so1 = xl1;
+                        succ = 0;
+                        t0 = t_step;
+                    } else {                                                  // :266-275
+                        succ++;
+                        xl0 = x0; xl1 = x1;
+                        so0 = x0; so1 = x1;
                         if (succ >= a.inc_steps) { succ = 0; dt *= 2.0f; }
                     }
                     stepidx++;
@@ -885,14 +1180,109 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval3(int n, TableWS *ws, const 
     }
 }
 
+// v8 LU standalone: the structural pattern of a row is its non-zero entries
+__global__ void __launch_bounds__(WG_THREADS) k_cgesv8(int n, const cf *__restrict__ A, const cf *__restrict__ B,
+                                                       cf *__restrict__ X) {
+    __shared__ LUBuf s_lu[2 * WAVES_PER_WG];
+    const int lane = lane_id();
+    const int r = lane & 31;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 2 + (lane >> 5);
+    const bool ok = sys < n && r < NV;
+    cf rA[NV];
+    uint32_t pat = 0;
+#pragma unroll
+    for (int c = 0; c < NV; c++) {
+        rA[c] = ok ? A[((size_t)sys * NV + r) * NV + c] : cmk(0.0f, 0.0f);
+        if (rA[c].x != 0.0f || rA[c].y != 0.0f) pat |= 1u << c;   // NaN counts as non-zero
+    }
+    const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
+    const cf x = lu_solve3s(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)]);
+    if (ok) X[(size_t)sys * NV + r] = x;
+}
+
+// v4 component kernels: one system / evaluation point per 16-lane row
+__global__ void __launch_bounds__(WG_THREADS) k_cgesv4(int n, const cf *__restrict__ A, const cf *__restrict__ B,
+                                                       cf *__restrict__ X) {
+    __shared__ LUBuf s_lu[4 * WAVES_PER_WG];
+    const int lane = lane_id();
+    const int r = lane & 15;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 4 + (lane >> 4);
+    const bool ok = sys < n;
+    const bool v1 = r + QL < NV;
+    cf A0[NV], A1[NV];
+#pragma unroll
+    for (int c = 0; c < NV; c++) {
+        A0[c] = ok ? A[((size_t)sys * NV + r) * NV + c] : cmk(0.0f, 0.0f);
+        A1[c] = (ok && v1) ? A[((size_t)sys * NV + r + QL) * NV + c] : cmk(0.0f, 0.0f);
+    }
+    const cf b0 = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
+    const cf b1 = (ok && v1) ? B[(size_t)sys * NV + r + QL] : cmk(0.0f, 0.0f);
+    cf x0, x1;
+    lu_solve4(A0, A1, b0, b1, lane, s_lu[(threadIdx.x / WAVE) * 4 + (lane >> 4)], x0, x1);
+    if (ok) {
+        X[(size_t)sys * NV + r] = x0;
+        if (v1) X[(size_t)sys * NV + r + QL] = x1;
+    }
+}
+
+__global__ void __launch_bounds__(WG_THREADS) k_eval4(int n, TableWS *ws, const cf *__restrict__ X,
+                                                      const cf *__restrict__ P, const cf *__restrict__ D,
+                                                      cf *__restrict__ HX, cf *__restrict__ HT, cf *__restrict__ H) {
+    __shared__ uint2 s_hx3[HX3_SLOT_CAP * 32];
+    __shared__ uint2 s_ht3[HT_TERMS * 32];
+    __shared__ SlotLDS4 s_slot[4 * WAVES_PER_WG];
+    const TableWS2 *w2 = ws2_of(ws);
+    const TableWS3 *w3 = ws3_of(ws);
+    if (w3->status != 0) return;
+    const int hx_len = w3->hx_len;
+    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = rebase_p_offsets(w3->hx[i]);
+    for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = rebase_p_offsets(w3->ht[i]);
+    {
+        float *z = reinterpret_cast<float *>(s_slot);
+        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
+    }
+    __syncthreads();
+    const int lane = lane_id();
+    const int r = lane & 15;
+    const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 4 + (lane >> 4);
+    SlotLDS4 &S = s_slot[(threadIdx.x / WAVE) * 4 + (lane >> 4)];
+    const bool ok = sys < n;
+    const bool v1 = r + QL < NV;
+    if (ok) {
+        for (int i = r; i < 31; i += QL) S.x[i] = X[(size_t)sys * 31 + i];
+        for (int i = r; i < NPP; i += QL) { S.p[i] = P[(size_t)sys * NPP + i]; S.dif[i] = D[(size_t)sys * NPP + i]; }
+    }
+    const uint32_t map0[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
+    const uint32_t map1[3] = {w2->map[0][r + QL], w2->map[1][r + QL], w2->map[2][r + QL]};
+    wave_lds_sync();
+    cf A0[NV], A1[NV], t0, t1, h0, h1;
+    eval_hx4(A0, A1, s_hx3, hx_len, map0, map1, S, r);
+    eval_ht4(s_ht3, S, r, t0, t1);
+    eval_h4(s_ht3, S, r, h0, h1);
+    if (ok) {
+#pragma unroll
+        for (int c = 0; c < NV; c++) HX[((size_t)sys * NV + r) * NV + c] = A0[c];
+        HT[(size_t)sys * NV + r] = t0;
+        H[(size_t)sys * NV + r] = h0;
+        if (v1) {
+#pragma unroll
+            for (int c = 0; c < NV; c++) HX[((size_t)sys * NV + r + QL) * NV + c] = A1[c];
+            HT[(size_t)sys * NV + r + QL] = t1;
+            H[(size_t)sys * NV + r + QL] = h1;
+        }
+    }
+}
+
 // ---------------------------------------------------------------- host side
-// HC_TRIFOCAL_KERNEL=v1|v2 selects an earlier tracker generation (A/B
-// baselines); default v3 (two paths per wave, LDS-broadcast LU).
+// HC_TRIFOCAL_KERNEL=v1|v2|v3|v4 selects another tracker generation (A/B
+// baselines, all bit-identical); default v8 = v3 + the structurally sparse LU
+// (hc_lu3s.hpp).  v4: four paths per wave (hc_track4.hpp).
 static int kernel_version() {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("HC_TRIFOCAL_KERNEL");
-        v = (e && e[0] == 'v' && e[1] == '1') ? 1 : (e && e[0] == 'v' && e[1] == '2') ? 2 : 3;
+        v = (e && e[0] == 'v' && e[1] == '1') ? 1 : (e && e[0] == 'v' && e[1] == '2') ? 2
+          : (e && e[0] == 'v' && e[1] == '3') ? 3 : (e && e[0] == 'v' && e[1] == '4') ? 4 : 8;
     }
     return v;
 }
@@ -906,12 +1296,23 @@ static int v3_minwaves() {
     }
     return w;
 }
+// HC_TRIFOCAL_ORDER=natural: dequeue in batch-id order (A/B baseline); default
+// longest-track-first (abort mode always dequeues sample-major, so whole
+// hypotheses finish as early as possible)
+static bool path_order_ltf() {
+    static int o = -1;
+    if (o < 0) {
+        const char *e = getenv("HC_TRIFOCAL_ORDER");
+        o = (e && e[0] == 'n') ? 0 : 1;
+    }
+    return o == 1;
+}
 static size_t ws_bytes_needed() {
     return ((sizeof(TableWS) + 255) & ~(size_t)255) + ((sizeof(TableWS2) + 255) & ~(size_t)255) +
            ((sizeof(TableWS3) + 255) & ~(size_t)255);
 }
 
-static int grid_for(int waves_needed, const void *kernel) {
+static int grid_for(int waves_needed, const void *kernel, int wg_threads = WG_THREADS) {
     static std::mutex mu;
     static int cache_dev = -1, cache_blocks = 0, cache_cus = 0;
     static const void *cache_k = nullptr;
@@ -922,11 +1323,12 @@ static int grid_for(int waves_needed, const void *kernel) {
         if (dev != cache_dev || kernel != cache_k) {
             int cus = 0, per_cu = 0;
             if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return -1;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, WG_THREADS, 0) != hipSuccess) per_cu = 1;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, wg_threads, 0) != hipSuccess) per_cu = 1;
             cache_dev = dev; cache_k = kernel; cache_cus = cus; cache_blocks = per_cu < 1 ? 1 : per_cu;
         }
     }
-    const int want = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    const int wpg = wg_threads / WAVE;
+    const int want = (waves_needed + wpg - 1) / wpg;
     const int cap = cache_cus * cache_blocks;
     return want < cap ? want : cap;
 }
@@ -955,6 +1357,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     KArgs k{};
     k.num_paths = (int)paths;
+    k.ordered = (!abort_mode && path_order_ltf()) ? 1 : 0;
     k.max_steps = t->settings.max_steps;
     k.max_corr = t->settings.max_corrections;
     k.inc_steps = t->settings.delta_t_inc_steps;
@@ -973,11 +1376,15 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.ws3 = ws3_of(ws);
     const int ver = kernel_version();
     const bool w4 = v3_minwaves() == 4;
-    const void *kern = ver == 1   ? (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>)
+    const void *kern = ver == 8   ? (abort_mode ? (const void *)k_track2<true, 4, 8> : (const void *)k_track2<false, 4, 8>)
+                       : ver == 4 ? (abort_mode ? (const void *)k_track4<true> : (const void *)k_track4<false>)
+                       : ver == 1 ? (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>)
                        : ver == 2 ? (abort_mode ? (const void *)k_track2<true, 3, 2> : (const void *)k_track2<false, 3, 2>)
                        : w4       ? (abort_mode ? (const void *)k_track2<true, 4, 3> : (const void *)k_track2<false, 4, 3>)
                                   : (abort_mode ? (const void *)k_track2<true, 3, 3> : (const void *)k_track2<false, 3, 3>);
-    const int grid = grid_for(ver >= 2 ? (int)((paths + 1) / 2) : (int)paths, kern);
+    const int wg_threads = WG_THREADS;
+    const int grid = grid_for(ver == 4 ? (int)((paths + 3) / 4) : ver >= 2 ? (int)((paths + 1) / 2) : (int)paths,
+                              kern, wg_threads);
     if (grid <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
         k.num_edgels = ab->num_triplet_edgels;
@@ -987,7 +1394,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
         k.batch_index = ab->trifocal_sols_batch_index;
     }
     void *kargs[] = {&k};
-    g_last_hip_error = hipLaunchKernel(kern, dim3(grid), dim3(WG_THREADS), kargs, 0, s);
+    g_last_hip_error = hipLaunchKernel(kern, dim3(grid), dim3(wg_threads), kargs, 0, s);
     if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
     return launch_status(HC_ERROR_LAUNCH);
 }
@@ -1032,7 +1439,15 @@ hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, h
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
     (void)hipGetLastError();
-    if (hc::kernel_version() == 3) {
+    if (hc::kernel_version() == 8) {
+        const int per = 2 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_cgesv8, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+                           (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+    } else if (hc::kernel_version() == 4) {
+        const int per = 4 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_cgesv4, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+                           (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+    } else if (hc::kernel_version() == 3) {
         const int per = 2 * hc::WAVES_PER_WG;
         hipLaunchKernelGGL(hc::k_cgesv3, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
                            (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
@@ -1060,7 +1475,12 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
     if ((hc::g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
     hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(64), 0, s, unified_index, ws, nullptr);
     if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-    if (hc::kernel_version() == 3) {
+    if (hc::kernel_version() == 4) {
+        const int per = 4 * hc::WAVES_PER_WG;
+        hipLaunchKernelGGL(hc::k_eval4, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
+                           (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
+                           (hc::cf *)H);
+    } else if (hc::kernel_version() == 3 || hc::kernel_version() == 8) {
         const int per = 2 * hc::WAVES_PER_WG;
         hipLaunchKernelGGL(hc::k_eval3, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
                            (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
@@ -1084,6 +1504,8 @@ const char *hc_trifocal_version(void) {
     switch (hc::kernel_version()) {
     case 1: return "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
     case 2: return "hc_trifocal gfx950 v2 (2 paths/wave, bpermute LU, per-lane term lists)";
+    case 8: return "hc_trifocal gfx950 v8 (2 paths/wave, structurally sparse LDS-broadcast LU, packed evals, 4 waves/SIMD)";
+    case 4: return "hc_trifocal gfx950 v4 (4 paths/wave, 2 rows/lane, LDS-broadcast LU, packed evals, 2 waves/SIMD)";
     default:
         return hc::v3_minwaves() == 4 ? "hc_trifocal gfx950 v3.1 (2 paths/wave, LDS-broadcast LU, permlane16 pivot search, packed evals, 4 waves/SIMD)"
                                       : "hc_trifocal gfx950 v3.1 (2 paths/wave, LDS-broadcast LU, permlane16 pivot search, packed evals, 3 waves/SIMD)";

@@ -52,7 +52,10 @@ struct alignas(16) SlotLDS {
     cf dif[NPP];     // diff params
     cf ent[NV * 7];  // dH/dx entries of row r at [r*7 + slot], slot 6 = 0
     SlotState st;
+    char bank_pad[16];   // slot stride = 16 mod 256 B: the slots of one wave (same offsets,
+                         // different bases) land on different LDS banks
 };
+static_assert(sizeof(SlotLDS) % 256 == 16, "SlotLDS stride must shift the LDS banks by 4 per slot");
 
 __device__ __forceinline__ float bperm_f(float v, int src_lane) {
     return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
