@@ -97,9 +97,20 @@ __device__ __forceinline__ void lu3s_update(cf (&rA)[NV], const cf &l, bool belo
     }
 }
 
+// reciprocals (o1, o2) of the cuCdivf factors of the pivot a lane owns, kept
+// from the forward step that chose it (brs, bis = pivot * o1 are recomputed
+// from the pivot element, which stays in the owner's rA)
+struct PivF { pf2 oo; };
+
+// s in the fast reciprocal range [2^-90, 2^120), on the bit pattern of a
+// non-negative float (NaN and the -1 "no candidate" key fall outside)
+__device__ __forceinline__ bool rcp_fast_bits(int bits) {
+    return (uint32_t)(bits - 0x12800000) < (uint32_t)(0x7B800000 - 0x12800000);
+}
+
 template <int I>
 __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool all_dense,
-                                             int lane, int r, int hb, bool row_lane, LUBuf &L) {
+                                             int lane, int r, int hb, bool row_lane, PivF &my, LUBuf &L) {
     if constexpr (I < NV) {
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
         const bool elig = rowid >= I && row_lane;
@@ -137,7 +148,7 @@ __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, u
         const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
         constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
         // a pivot outside the fast reciprocal range (tiny, zero, NaN) makes the step dense
-        const bool dense = all_dense || __builtin_amdgcn_ballot_w64(!rcp_fast_ok(piv_abs)) != 0ull;
+        const bool dense = all_dense || __builtin_amdgcn_ballot_w64(!rcp_fast_bits(__float_as_int(piv_abs))) != 0ull;
         const uint32_t pmw = dense ? FULL : ((pp0 | pp1) & FULL);
         if (is_piv) {                                          // pivot row -> buffer
             L.row[I] = rA[I];
@@ -152,15 +163,22 @@ __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, u
         const int piv_pos = __float_as_int(pr.x);
         if (is_piv) rowid = I;                                 // :70-82
         else if (rowid == I) rowid = piv_pos;
+        // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
+        // for its position of the back substitution (same inputs, same ops as
+        // recomputing them there from its rA[I], which no later step changes)
         cf reg;
+        divf f;
         if (__builtin_expect(!dense, 1)) {
-            const float s = __builtin_fabsf(sxi.x) + __builtin_fabsf(sxi.y);   // == piv_abs, in range
-            const divf f = cdiv_factors_fast(sxi, s);
+            f = cdiv_factors_fast(sxi, piv_abs);               // piv_abs == |sxi.re| + |sxi.im|, in range
             reg = cmk((f.o1 * f.brs) * f.o2, (-(f.o1 * f.bis)) * f.o2);
         } else {
-            const divf f = cdiv_factors(sxi);
+            f = cdiv_factors(sxi);
             reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
         }
+        if (is_piv) my.oo = pf2{f.o1, f.o2};
+        // opaque: the select chain must be resolved here, not carried as 30
+        // per-step factor pairs into the back substitution
+        asm volatile("" : "+v"(my.oo));
         const bool below = rowid > I;                          // :86-93
         cf l = cmk(0.0f, 0.0f);
         if (below) {
@@ -174,7 +192,40 @@ __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, u
         // after a dense step (l may be non-finite) nothing is known zero
         if (below && (dense || ((pat >> I) & 1u))) pat |= dense ? 0xFFFFFFFFu : pmw;
         lu3s_update<I + 1>(rA, l, below, pmw, L);
-        lu3s_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, L);
+        lu3s_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+    }
+}
+
+// cdiv_apply(b, f) = cuCdivf(b, pivot) in packed FP32, op for op:
+// (brs, bis) = pivot*o1; (ars, ais) = b*o1; re = (ars*brs + ais*bis)*o2; im = (ais*brs - ars*bis)*o2
+__device__ __forceinline__ pf2 pcdiv_apply(pf2 b, pf2 piv, const PivF &f) {
+    pf2 bb, a, t1, t2, s, q;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(bb) : "v"(piv), "v"(f.oo));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(a) : "v"(b), "v"(f.oo));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t1) : "v"(a), "v"(bb));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1]" : "=v"(t2) : "v"(a), "v"(bb));
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(s) : "v"(t1), "v"(t2));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(q) : "v"(s), "v"(f.oo));
+    return q;
+}
+
+// back substitution (:97-106): the lane with final rowid == I owns position I
+// and divides its right-hand side by its pivot with the factors kept in the
+// forward pass; x_I is published through the buffer
+template <int I>
+__device__ __forceinline__ void lu3s_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, LUBuf &L) {
+    if constexpr (I >= 0) {
+        if (rowid == I) {
+            const pf2 q = pcdiv_apply(pf2{rB.x, rB.y}, pf2{rA[I].x, rA[I].y}, my);
+            L.row[I] = cmk(q.x, q.y);
+        }
+        wave_lds_sync();
+        const cf xi = L.row[I];
+        if (rowid < I) {
+            const pf2 v = pcmsub(pf2{rB.x, rB.y}, pf2{xi.x, xi.y}, pf2{rA[I].x, rA[I].y});
+            rB = cmk(v.x, v.y);
+        }
+        lu3s_backward<I - 1>(rA, rB, rowid, my, L);
     }
 }
 
@@ -189,8 +240,9 @@ __device__ __forceinline__ cf lu_solve3s(cf (&rA)[NV], cf rB, int lane, uint32_t
     const bool row_lane = r < NV;
     int rowid = row_lane ? r : 99;   // padding lanes never pivot
     uint32_t pat = row_lane ? pattern : 0u;
-    lu3s_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, L);
-    lu3_backward<NV - 1>(rA, rB, rowid, L);
+    PivF my{pf2{0.0f, 0.0f}};
+    lu3s_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+    lu3s_backward<NV - 1>(rA, rB, rowid, my, L);
     wave_lds_sync();
     return L.row[row_lane ? r : 0];
 }
