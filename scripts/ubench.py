@@ -80,6 +80,20 @@ def main():
     out["track_ms"] = ms
     out["track_stages"] = stages
     out["track_ns_per_stage"] = ms * 1e6 / stages
+    # latency: one RANSAC sample (312 paths, < 1 wave per CU) -- the launch lasts
+    # as long as its longest path (same stage count for every bit-identical build)
+    r1 = tr.allocate(1)
+    t1, d1 = tt[:1].contiguous(), dd[:1].contiguous()
+
+    def run1():
+        tr.reset_tracks(r1)
+        tr.launch(t1, d1, r1)
+    ms1 = timeit(run1)
+    h1 = r1.host()
+    st1 = h1["stats"]["steps"] * 4 + h1["stats"]["corrections"]
+    out["track1_ms"] = ms1
+    out["track1_max_stages"] = int(st1.max())
+    out["track1_us_per_stage"] = ms1 * 1e3 / int(st1.max())
     out["version"] = L.hc_trifocal_version().decode()
     print(json.dumps(out))
 

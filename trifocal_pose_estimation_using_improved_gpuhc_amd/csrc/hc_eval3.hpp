@@ -75,28 +75,56 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
     return r;
 }
 
-// dH/dx: row r of both paths' Jacobians into rA
+// Software-pipelined term loops.  Every term's table word is read up front
+// (the Jacobian registers are dead while the evaluations run), and a term's
+// operand reads are issued EV_AHEAD terms before it is computed, in program
+// order ahead of the previous terms' entry stores (which the compiler may not
+// move loads across), so a lane has several terms' LDS reads in flight instead
+// of one round trip per term.
+constexpr int EV_AHEAD = 2;
+
+struct HxOps { pf2 pa, pb, xu, xv; };
+__device__ __forceinline__ HxOps hx_ops(const char *sb, uint2 w) {
+    return HxOps{ldp(sb, w.x & 0xFFFFu), ldp(sb, w.x >> 16), ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu)};
+}
+
+// the term loop of eval_hx3: operands are read through sb (x, p of the slot),
+// running sums written through eb (the lane's entry row)
+__device__ __forceinline__ void eval_hx3_terms(const uint2 *s_hx3, const char *sb, char *eb, int r) {
+    uint2 w[HX3_SLOT_CAP];
+#pragma unroll
+    for (int k = 0; k < HX3_SLOT_CAP; k++) w[k] = s_hx3[k * 32 + r];
+    HxOps o[EV_AHEAD + 1];
+#pragma unroll
+    for (int k = 0; k < EV_AHEAD; k++) o[k] = hx_ops(sb, w[k]);
+    pf2 acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int k = 0; k < HX3_SLOT_CAP; k++) {
+        if (k + EV_AHEAD < HX3_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
+        const HxOps &q = o[k % (EV_AHEAD + 1)];
+        const float co = (float)(int)(int8_t)(uint8_t)(w[k].y >> 16);
+        pf2 P = q.pa * pf2{co, co};
+        P = pcmul(P, q.pb);
+        P = pcmul(P, q.xu);
+        acc = pcmadd(acc, P, q.xv);
+        const bool last = (int)w[k].y < 0;   // last term of an entry (never set on padding terms)
+        *reinterpret_cast<pf2 *>(eb + (last ? ((w[k].y >> 24) & 0x7Fu) : 8u * 6u)) = acc;
+        acc = last ? pf2{0.0f, 0.0f} : acc;
+    }
+}
+
+// dH/dx: row r of both paths' Jacobians into rA.  The term loop is fully
+// unrolled over the padded table (HX3_SLOT_CAP words per lane; the caller stages
+// all of them) and branch-free, so the scheduler can keep several terms' LDS
+// reads in flight: every term stores its running sum -- to its entry slot when
+// it is the entry's last term, else to the lane's structural-zero slot 6 as a
+// scratch word -- and slot 6 is re-zeroed before the gather.
 __device__ __forceinline__ void eval_hx3(cf (&rA)[NV], const uint2 *s_hx3, int hx_len, const uint32_t (&map)[3],
                                          SlotLDS &S, int r) {
-    const char *sb = reinterpret_cast<const char *>(&S);
+    (void)hx_len;
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
-    char *eb = reinterpret_cast<char *>(ent_row);
+    eval_hx3_terms(s_hx3, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
     if (r < NV) ent_row[6] = cmk(0.0f, 0.0f);   // structural zero (the v3 LU reuses this block)
-    pf2 acc = {0.0f, 0.0f};
-    for (int k = 0; k < hx_len; k++) {
-        const uint2 w = s_hx3[k * 32 + r];
-        const pf2 pa = ldp(sb, w.x & 0xFFFFu), pb = ldp(sb, w.x >> 16);
-        const pf2 xu = ldp(sb, w.y & 0xFFu), xv = ldp(sb, (w.y >> 8) & 0xFFu);
-        const float co = (float)(int)(int8_t)(uint8_t)(w.y >> 16);
-        pf2 P = pa * pf2{co, co};
-        P = pcmul(P, pb);
-        P = pcmul(P, xu);
-        acc = pcmadd(acc, P, xv);
-        if ((int)w.y < 0) {             // last term of an entry (never set on padding terms)
-            *reinterpret_cast<pf2 *>(eb + ((w.y >> 24) & 0x7Fu)) = acc;
-            acc = pf2{0.0f, 0.0f};
-        }
-    }
     wave_lds_sync();
 #pragma unroll
     for (int c = 0; c < NV; c++) {
@@ -105,39 +133,60 @@ __device__ __forceinline__ void eval_hx3(cf (&rA)[NV], const uint2 *s_hx3, int h
     }
 }
 
+struct HtOps { pf2 pa, pb, da, db, xu, xv, xw; };
+__device__ __forceinline__ HtOps ht_ops(const char *sb, uint2 w) {
+    const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
+    return HtOps{ldp(sb, oa), ldp(sb, ob), ldp(sb + SLOT_DIF_DELTA, oa), ldp(sb + SLOT_DIF_DELTA, ob),
+                 ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu), ldp(sb, (w.y >> 16) & 0xFFu)};
+}
+
 // dH/dt: b = -sum_j c*(d[a]*p[b] + d[b]*p[a])*x[u]*x[v]*x[w]
 __device__ __forceinline__ cf eval_ht3(const uint2 *s_ht3, const SlotLDS &S, int r) {
     const char *sb = reinterpret_cast<const char *>(&S);
+    uint2 w[HT_TERMS];
+#pragma unroll
+    for (int j = 0; j < HT_TERMS; j++) w[j] = s_ht3[j * 32 + r];
+    HtOps o[EV_AHEAD + 1];
+#pragma unroll
+    for (int j = 0; j < EV_AHEAD; j++) o[j] = ht_ops(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
     for (int j = 0; j < HT_TERMS; j++) {
-        const uint2 w = s_ht3[j * 32 + r];
-        const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
-        const pf2 pa = ldp(sb, oa), pb = ldp(sb, ob);
-        const pf2 da = ldp(sb + SLOT_DIF_DELTA, oa), db = ldp(sb + SLOT_DIF_DELTA, ob);
-        const pf2 xu = ldp(sb, w.y & 0xFFu), xv = ldp(sb, (w.y >> 8) & 0xFFu), xw = ldp(sb, (w.y >> 16) & 0xFFu);
-        const float co = (float)((int)w.y >> 24);
-        pf2 s = pcmadd(pcmul(da, pb), db, pa);
+        if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = ht_ops(sb, w[j + EV_AHEAD]);
+        const HtOps &q = o[j % (EV_AHEAD + 1)];
+        const float co = (float)((int)w[j].y >> 24);
+        pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
         s = s * pf2{co, co};
-        const pf2 P = pcmul(pcmul(s, xu), xv);
-        acc = pcmsub(acc, P, xw);
+        const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
+        acc = pcmsub(acc, P, q.xw);
     }
     return cmk(acc.x, acc.y);
+}
+
+struct HOps { pf2 pa, pb, xu, xv, xw; };
+__device__ __forceinline__ HOps h_ops(const char *sb, uint2 w) {
+    return HOps{ldp(sb, w.x & 0xFFFFu), ldp(sb, w.x >> 16), ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu),
+                ldp(sb, (w.y >> 16) & 0xFFu)};
 }
 
 // H: b = sum_j c*p[a]*p[b]*x[u]*x[v]*x[w]
 __device__ __forceinline__ cf eval_h3(const uint2 *s_ht3, const SlotLDS &S, int r) {
     const char *sb = reinterpret_cast<const char *>(&S);
+    uint2 w[HT_TERMS];
+#pragma unroll
+    for (int j = 0; j < HT_TERMS; j++) w[j] = s_ht3[j * 32 + r];
+    HOps o[EV_AHEAD + 1];
+#pragma unroll
+    for (int j = 0; j < EV_AHEAD; j++) o[j] = h_ops(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
-#pragma unroll 4
+#pragma unroll
     for (int j = 0; j < HT_TERMS; j++) {
-        const uint2 w = s_ht3[j * 32 + r];
-        const pf2 pa = ldp(sb, w.x & 0xFFFFu), pb = ldp(sb, w.x >> 16);
-        const pf2 xu = ldp(sb, w.y & 0xFFu), xv = ldp(sb, (w.y >> 8) & 0xFFu), xw = ldp(sb, (w.y >> 16) & 0xFFu);
-        const float co = (float)((int)w.y >> 24);
-        pf2 P = pa * pf2{co, co};
-        P = pcmul(pcmul(pcmul(P, pb), xu), xv);
-        acc = pcmadd(acc, P, xw);
+        if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = h_ops(sb, w[j + EV_AHEAD]);
+        const HOps &q = o[j % (EV_AHEAD + 1)];
+        const float co = (float)((int)w[j].y >> 24);
+        pf2 P = q.pa * pf2{co, co};
+        P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
+        acc = pcmadd(acc, P, q.xw);
     }
     return cmk(acc.x, acc.y);
 }

@@ -458,6 +458,13 @@ __device__ __forceinline__ int half_sum_i(int v) {
     return v;
 }
 
+#ifdef HC_DIAG_PHASES
+// diagnostic build: per-phase shader cycles summed over waves (k_track2):
+// [0] slot phases, [1] park + p(t), [2] dH/dx, [3] dH/dt | H, [4] LU forward,
+// [5] LU backward, [6] stage update, [7] wave lifetime, [8] waves
+__device__ unsigned long long g_diag_phase[9];
+#endif
+
 template <bool ABORT, int MINW, int V>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     // V = 2: bpermute LU + v2 evals; V = 3: LDS-broadcast LU + packed v3 evals;
@@ -478,7 +485,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     uint2 *s_hx3 = reinterpret_cast<uint2 *>(s_tab);
     uint2 *s_ht3 = s_hx3 + HX3_SLOT_CAP * 32;
     if constexpr (EV3) {
-        for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];
+        for (int i = threadIdx.x; i < HX3_SLOT_CAP * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];   // padded table
         for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = w3->ht[i];
     } else {
         for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx2[i] = w2->hx[i];
@@ -504,12 +511,23 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
 
     // per-slot state (uniform within a half)
     int ph = PH_DEQ, b = -1, smp_loaded = -1;
+#ifdef HC_DIAG_TIMES
+    int diag_t0 = 0;
+#endif
     int s = 0, stepidx = 0, coef = 1, succ = 0, nsteps = 0, ncorr = 0;
     float t0 = 0.0f, t_step = 0.0f, dt = 0.01f, h2 = 0.0f, scale = 0.0f;
     bool end_zone = false, check = true, isSucc = false, isInf = false;
     cf x = cmk(0.0f, 0.0f), xl = x, sols = x;
 
+#ifdef HC_DIAG_PHASES
+    uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t dt_ = __builtin_amdgcn_s_memtime(), dt0_ = dt_;
+#define HC_DIAG_MARK(k) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); dg[k] += n_ - dt_; dt_ = n_; } while (0)
+#else
+#define HC_DIAG_MARK(k) do { } while (0)
+#endif
     for (;;) {
+        HC_DIAG_MARK(6);
         // ---------------- resolve slot phases until every slot is at a stage or idle
         for (;;) {
             if (ph == PH_FINISH) {                                            // :282-286
@@ -563,6 +581,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
                 if (r == 0) {
                     a.conv[b] = conv ? 1 : 0;
                     a.inf[b] = isInf ? 1 : 0;
+#ifdef HC_DIAG_TIMES
+                    // diagnostic build: dequeue / finish device timestamps (100 MHz) of each path
+                    in21 = diag_t0;
+                    in31 = (int)__builtin_amdgcn_s_memrealtime();
+#endif
                     if (a.stats) a.stats[b] = hcPathStats{nsteps, ncorr, in21, in31};
                 }
                 ph = PH_DEQ;
@@ -597,6 +620,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
                             S.dif[r + 32] = a.diff_params[(size_t)smp * NPP + r + 32];
                         }
                         smp_loaded = smp;
+#ifdef HC_DIAG_TIMES
+                        diag_t0 = (int)__builtin_amdgcn_s_memrealtime();
+#endif
                         const cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
                         const cf *dstart = a.start_sols_array ? a.start_sols_array[trk]
                                                               : a.start_sols + (size_t)trk * (NV + 1);
@@ -640,6 +666,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
             if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
         }
         if (__ballot(ph == PH_STAGE) == 0ull) break;
+        HC_DIAG_MARK(0);
 
         // ---------------- one stage for both slots
         // park the slot state in LDS so it does not occupy VGPRs across eval + LU
@@ -672,9 +699,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
         const int r_v = lane_v & 31;
         const bool act = ph_in == PH_STAGE;
         const bool pred = act && s_in < 4;
-        cf rA[NV];
-        if constexpr (EV3) eval_hx3(rA, s_hx3, hx_len, map, S, r_v);     // :184 / :220
-        else eval_hx2(rA, s_hx2, hx_len, map, S, r_v);
+        HC_DIAG_MARK(1);
+        // right-hand side first: dH/dt | H need no Jacobian registers, so their
+        // LDS gathers can run many terms ahead
         cf rB = cmk(0.0f, 0.0f);
         if (__ballot(pred) != 0ull) {                                        // :185
             const cf t = EV3 ? eval_ht3(s_ht3, S, r_v) : eval_ht2(s_ht, S, r_v);
@@ -684,12 +711,22 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
             const cf t = EV3 ? eval_h3(s_ht3, S, r_v) : eval_h2(s_ht, S, r_v);
             if (!pred) rB = t;
         }
+        HC_DIAG_MARK(3);
+        cf rA[NV];
+        if constexpr (EV3) eval_hx3(rA, s_hx3, hx_len, map, S, r_v);     // :184 / :220
+        else eval_hx2(rA, s_hx2, hx_len, map, S, r_v);
         wave_lds_sync();
+        HC_DIAG_MARK(2);
         cf k;                                                                // :188 / :224
+#ifdef HC_DIAG_PHASES
+        if constexpr (V == 8) { uint64_t tm_; k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent), &tm_); dg[4] += tm_ - dt_; dt_ = tm_; }
+        else
+#endif
         if constexpr (V == 8) k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));
         else if constexpr (V == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
         else k = lu_solve2(rA, rB, lane_v);
         wave_lds_sync();
+        HC_DIAG_MARK(5);
         {
             const SlotState q = S.st;
             t0 = q.t0; t_step = q.t_step; dt = q.dt; h2 = q.h2; scale = q.scale;
@@ -751,6 +788,15 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
             }
         }
     }
+#ifdef HC_DIAG_PHASES
+    HC_DIAG_MARK(0);
+    if (lane == 0) {
+        dg[7] = __builtin_amdgcn_s_memtime() - dt0_;
+        for (int q = 0; q < 8; q++) atomicAdd(&g_diag_phase[q], (unsigned long long)dg[q]);
+        atomicAdd(&g_diag_phase[8], 1ull);
+    }
+#endif
+#undef HC_DIAG_MARK
 }
 
 // ---------------------------------------------------------------- tracker v4
@@ -1148,7 +1194,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval3(int n, TableWS *ws, const 
     const TableWS3 *w3 = ws3_of(ws);
     if (w3->status != 0) return;
     const int hx_len = w3->hx_len;
-    for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];
+    for (int i = threadIdx.x; i < HX3_SLOT_CAP * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];   // padded table
     for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = w3->ht[i];
     {
         float *z = reinterpret_cast<float *>(s_slot);
@@ -1402,6 +1448,16 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
 }  // namespace hc
 
 extern "C" {
+#ifdef HC_DIAG_PHASES
+int hc_diag_phases(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_phase), sizeof(unsigned long long) * 9) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 size_t hc_trifocal_workspace_size(void) { return hc::ws_bytes_needed(); }
 

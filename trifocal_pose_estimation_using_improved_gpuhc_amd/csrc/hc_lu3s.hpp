@@ -229,7 +229,8 @@ __device__ __forceinline__ void lu3s_backward(const cf (&rA)[NV], cf &rB, int ro
     }
 }
 
-__device__ __forceinline__ cf lu_solve3s(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L) {
+__device__ __forceinline__ cf lu_solve3s(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L,
+                                        uint64_t *t_mid = nullptr) {
     // every entry finite and below 2^88 in magnitude (NaN fails the compare)
     bool ok = true;
 #pragma unroll
@@ -242,6 +243,7 @@ __device__ __forceinline__ cf lu_solve3s(cf (&rA)[NV], cf rB, int lane, uint32_t
     uint32_t pat = row_lane ? pattern : 0u;
     PivF my{pf2{0.0f, 0.0f}};
     lu3s_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+    if (t_mid) *t_mid = __builtin_amdgcn_s_memtime();   // diagnostic builds only
     lu3s_backward<NV - 1>(rA, rB, rowid, my, L);
     wave_lds_sync();
     return L.row[row_lane ? r : 0];
