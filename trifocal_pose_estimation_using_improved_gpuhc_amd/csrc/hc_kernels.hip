@@ -15,6 +15,7 @@
 #include "hc_lu3.hpp"
 #include "hc_track4.hpp"
 #include "hc_lu3s.hpp"
+#include "hc_lu9.hpp"
 #include "../../include/hc_trifocal.h"
 
 #include <atomic>
@@ -461,8 +462,10 @@ __device__ __forceinline__ int half_sum_i(int v) {
 #ifdef HC_DIAG_PHASES
 // diagnostic build: per-phase shader cycles summed over waves (k_track2):
 // [0] slot phases, [1] park + p(t), [2] dH/dx, [3] dH/dt | H, [4] LU forward,
-// [5] LU backward, [6] stage update, [7] wave lifetime, [8] waves
-__device__ unsigned long long g_diag_phase[9];
+// [5] LU backward, [6] stage update, [7] wave lifetime, [8] waves; with
+// HC_DIAG_LU the forward steps' parts [9] pivot search, [10] row broadcast,
+// [11] reciprocal + multipliers, [12] rank-1 update
+__device__ unsigned long long g_diag_phase[13];
 #endif
 
 template <bool ABORT, int MINW, int V>
@@ -505,7 +508,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     if (r == 30) S.x[30] = cmk(1.0f, 0.0f);
     if (r == 0) S.p[33] = cmk(1.0f, 0.0f);
     const uint32_t map[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
-    const uint32_t row_pat = V == 8 ? row_pattern(map) : 0u;   // structural pattern of row r (v8 LU)
+    const uint32_t row_pat = V >= 8 ? row_pattern(map) : 0u;   // structural pattern of row r (v8 LU)
     const bool rl = r < NV;
     wave_lds_sync();
 
@@ -521,6 +524,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
 
 #ifdef HC_DIAG_PHASES
     uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef HC_DIAG_LU
+    uint64_t lgd[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#else
+    uint64_t *lgd = nullptr;
+#endif
     uint64_t dt_ = __builtin_amdgcn_s_memtime(), dt0_ = dt_;
 #define HC_DIAG_MARK(k) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); dg[k] += n_ - dt_; dt_ = n_; } while (0)
 #else
@@ -719,10 +727,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
         HC_DIAG_MARK(2);
         cf k;                                                                // :188 / :224
 #ifdef HC_DIAG_PHASES
-        if constexpr (V == 8) { uint64_t tm_; k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent), &tm_); dg[4] += tm_ - dt_; dt_ = tm_; }
+        if constexpr (V == 8) { uint64_t tm_; k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent), &tm_, lgd); dg[4] += tm_ - dt_; dt_ = tm_; }
         else
 #endif
-        if constexpr (V == 8) k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));
+        if constexpr (V == 9) k = lu_solve9<LU9_PROD>(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));
+        else if constexpr (V == 8) k = lu_solve3s(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));
         else if constexpr (V == 3) k = lu_solve3(rA, rB, lane_v, *reinterpret_cast<LUBuf *>(S.ent));
         else k = lu_solve2(rA, rB, lane_v);
         wave_lds_sync();
@@ -794,6 +803,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
         dg[7] = __builtin_amdgcn_s_memtime() - dt0_;
         for (int q = 0; q < 8; q++) atomicAdd(&g_diag_phase[q], (unsigned long long)dg[q]);
         atomicAdd(&g_diag_phase[8], 1ull);
+#ifdef HC_DIAG_LU
+        for (int q = 0; q < 4; q++) atomicAdd(&g_diag_phase[9 + q], (unsigned long long)lgd[q]);
+#endif
     }
 #endif
 #undef HC_DIAG_MARK
@@ -1226,7 +1238,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval3(int n, TableWS *ws, const 
     }
 }
 
-// v8 LU standalone: the structural pattern of a row is its non-zero entries
+// v8 / v9 LU standalone: the structural pattern of a row is its non-zero entries
+template <bool V9>
 __global__ void __launch_bounds__(WG_THREADS) k_cgesv8(int n, const cf *__restrict__ A, const cf *__restrict__ B,
                                                        cf *__restrict__ X) {
     __shared__ LUBuf s_lu[2 * WAVES_PER_WG];
@@ -1242,7 +1255,8 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv8(int n, const cf *__restri
         if (rA[c].x != 0.0f || rA[c].y != 0.0f) pat |= 1u << c;   // NaN counts as non-zero
     }
     const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
-    const cf x = lu_solve3s(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)]);
+    const cf x = V9 ? lu_solve9<LU9_PROD>(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)])
+                    : lu_solve3s(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)]);
     if (ok) X[(size_t)sys * NV + r] = x;
 }
 
@@ -1320,15 +1334,17 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval4(int n, TableWS *ws, const 
 }
 
 // ---------------------------------------------------------------- host side
-// HC_TRIFOCAL_KERNEL=v1|v2|v3|v4 selects another tracker generation (A/B
-// baselines, all bit-identical); default v8 = v3 + the structurally sparse LU
-// (hc_lu3s.hpp).  v4: four paths per wave (hc_track4.hpp).
+// HC_TRIFOCAL_KERNEL=v1|v2|v3|v4|v8 selects another tracker generation (A/B
+// baselines, all bit-identical); default v9 = v3 evals + the structurally
+// sparse LU with lean pivot steps (hc_lu9.hpp); v8 = the sparse LU of
+// hc_lu3s.hpp.  v4: four paths per wave (hc_track4.hpp).
 static int kernel_version() {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("HC_TRIFOCAL_KERNEL");
         v = (e && e[0] == 'v' && e[1] == '1') ? 1 : (e && e[0] == 'v' && e[1] == '2') ? 2
-          : (e && e[0] == 'v' && e[1] == '3') ? 3 : (e && e[0] == 'v' && e[1] == '4') ? 4 : 8;
+          : (e && e[0] == 'v' && e[1] == '3') ? 3 : (e && e[0] == 'v' && e[1] == '4') ? 4
+          : (e && e[0] == 'v' && e[1] == '8') ? 8 : 9;
     }
     return v;
 }
@@ -1422,7 +1438,8 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.ws3 = ws3_of(ws);
     const int ver = kernel_version();
     const bool w4 = v3_minwaves() == 4;
-    const void *kern = ver == 8   ? (abort_mode ? (const void *)k_track2<true, 4, 8> : (const void *)k_track2<false, 4, 8>)
+    const void *kern = ver == 9   ? (abort_mode ? (const void *)k_track2<true, 4, 9> : (const void *)k_track2<false, 4, 9>)
+                       : ver == 8 ? (abort_mode ? (const void *)k_track2<true, 4, 8> : (const void *)k_track2<false, 4, 8>)
                        : ver == 4 ? (abort_mode ? (const void *)k_track4<true> : (const void *)k_track4<false>)
                        : ver == 1 ? (abort_mode ? (const void *)k_track<true> : (const void *)k_track<false>)
                        : ver == 2 ? (abort_mode ? (const void *)k_track2<true, 3, 2> : (const void *)k_track2<false, 3, 2>)
@@ -1450,9 +1467,9 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
 extern "C" {
 #ifdef HC_DIAG_PHASES
 int hc_diag_phases(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_phase), sizeof(unsigned long long) * 9) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_phase), sizeof(unsigned long long) * 13) != hipSuccess) return -1;
     if (reset) {
-        static const unsigned long long z[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+        static const unsigned long long z[13] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_phase), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
@@ -1495,9 +1512,10 @@ hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, h
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
     (void)hipGetLastError();
-    if (hc::kernel_version() == 8) {
+    if (hc::kernel_version() >= 8) {
         const int per = 2 * hc::WAVES_PER_WG;
-        hipLaunchKernelGGL(hc::k_cgesv8, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+        hipLaunchKernelGGL(hc::kernel_version() == 9 ? hc::k_cgesv8<true> : hc::k_cgesv8<false>,
+                           dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
                            (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
     } else if (hc::kernel_version() == 4) {
         const int per = 4 * hc::WAVES_PER_WG;
@@ -1560,6 +1578,7 @@ const char *hc_trifocal_version(void) {
     switch (hc::kernel_version()) {
     case 1: return "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
     case 2: return "hc_trifocal gfx950 v2 (2 paths/wave, bpermute LU, per-lane term lists)";
+    case 9: return "hc_trifocal gfx950 v9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and readlane back substitution, pipelined evals, 4 waves/SIMD)";
     case 8: return "hc_trifocal gfx950 v8 (2 paths/wave, structurally sparse LDS-broadcast LU, packed evals, 4 waves/SIMD)";
     case 4: return "hc_trifocal gfx950 v4 (4 paths/wave, 2 rows/lane, LDS-broadcast LU, packed evals, 2 waves/SIMD)";
     default:

@@ -108,9 +108,18 @@ __device__ __forceinline__ bool rcp_fast_bits(int bits) {
     return (uint32_t)(bits - 0x12800000) < (uint32_t)(0x7B800000 - 0x12800000);
 }
 
+// diagnostic builds (HC_DIAG_LU): shader cycles of the forward step's parts,
+// summed into lg[0..3]; lg[7] holds the last timestamp
+#ifdef HC_DIAG_LU
+#define LU_MARK(k) do { if (lg) { const uint64_t n_ = __builtin_amdgcn_s_memtime(); lg[k] += n_ - lg[7]; lg[7] = n_; } } while (0)
+#else
+#define LU_MARK(k) do { } while (0)
+#endif
+
 template <int I>
 __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool all_dense,
-                                             int lane, int r, int hb, bool row_lane, PivF &my, LUBuf &L) {
+                                             int lane, int r, int hb, bool row_lane, PivF &my, LUBuf &L,
+                                             uint64_t *lg) {
     if constexpr (I < NV) {
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
         const bool elig = rowid >= I && row_lane;
@@ -150,6 +159,7 @@ __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, u
         // a pivot outside the fast reciprocal range (tiny, zero, NaN) makes the step dense
         const bool dense = all_dense || __builtin_amdgcn_ballot_w64(!rcp_fast_bits(__float_as_int(piv_abs))) != 0ull;
         const uint32_t pmw = dense ? FULL : ((pp0 | pp1) & FULL);
+        LU_MARK(0);
         if (is_piv) {                                          // pivot row -> buffer
             L.row[I] = rA[I];
             lu3s_put_row<I + 1>(rA, pmw, L);
@@ -161,6 +171,7 @@ __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, u
         cf sB0, pr;
         ld4(&L.row[30], sB0, pr);
         const int piv_pos = __float_as_int(pr.x);
+        LU_MARK(1);
         if (is_piv) rowid = I;                                 // :70-82
         else if (rowid == I) rowid = piv_pos;
         // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
@@ -191,8 +202,10 @@ __device__ __forceinline__ void lu3s_forward(cf (&rA)[NV], cf &rB, int &rowid, u
         // patterns (both halves': a superset of its own pivot row's, one VALU op);
         // after a dense step (l may be non-finite) nothing is known zero
         if (below && (dense || ((pat >> I) & 1u))) pat |= dense ? 0xFFFFFFFFu : pmw;
+        LU_MARK(2);
         lu3s_update<I + 1>(rA, l, below, pmw, L);
-        lu3s_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+        LU_MARK(3);
+        lu3s_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L, lg);
     }
 }
 
@@ -230,7 +243,7 @@ __device__ __forceinline__ void lu3s_backward(const cf (&rA)[NV], cf &rB, int ro
 }
 
 __device__ __forceinline__ cf lu_solve3s(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L,
-                                        uint64_t *t_mid = nullptr) {
+                                        uint64_t *t_mid = nullptr, uint64_t *lg = nullptr) {
     // every entry finite and below 2^88 in magnitude (NaN fails the compare)
     bool ok = true;
 #pragma unroll
@@ -242,7 +255,10 @@ __device__ __forceinline__ cf lu_solve3s(cf (&rA)[NV], cf rB, int lane, uint32_t
     int rowid = row_lane ? r : 99;   // padding lanes never pivot
     uint32_t pat = row_lane ? pattern : 0u;
     PivF my{pf2{0.0f, 0.0f}};
-    lu3s_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+#ifdef HC_DIAG_LU
+    if (lg) lg[7] = __builtin_amdgcn_s_memtime();
+#endif
+    lu3s_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L, lg);
     if (t_mid) *t_mid = __builtin_amdgcn_s_memtime();   // diagnostic builds only
     lu3s_backward<NV - 1>(rA, rB, rowid, my, L);
     wave_lds_sync();
