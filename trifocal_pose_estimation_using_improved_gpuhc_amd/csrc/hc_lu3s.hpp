@@ -33,7 +33,7 @@
 namespace hc {
 
 #ifndef HC_LU3S_CHUNK
-#define HC_LU3S_CHUNK 6
+#define HC_LU3S_CHUNK 4
 #endif
 constexpr int LU3S_CHUNK = HC_LU3S_CHUNK;   // columns per skippable group (even)
 
