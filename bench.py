@@ -57,6 +57,10 @@ def parse():
     ap.add_argument("--noisy-trials", type=int, default=10,
                     help="config 5: RANSAC runs on sigma=1px noisy synthcurves (pose success rate); 0 disables")
     ap.add_argument("--noisy-sigma", type=float, default=1.0)
+    ap.add_argument("--streams", type=int, default=2,
+                    help="HIP streams the timed steps rotate over: step i runs on stream i %% streams with its own "
+                         "track buffers and workspace, so one batch's tail overlaps the next batch's start "
+                         "(1 = strictly serial launches)")
     return ap.parse_args()
 
 
@@ -92,30 +96,48 @@ def main():
     res = tr.allocate(S, stats=True)
     stream = torch.cuda.current_stream(dev)
 
-    def step():
-        tr.reset_tracks(res)
-        tr.launch(tgt, dif, res, stream=stream)
+    # step i: batch i on stream i % NS with its own buffers and workspace (independent
+    # RANSAC batches; a stream reuses its buffers only after its previous launch)
+    NS = max(1, args.streams)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(NS - 1)]
+    bufs = [res] + [tr.allocate(S, stats=True) for _ in range(NS - 1)]
+    wss = [tr.workspace] + [tr.new_workspace() for _ in range(NS - 1)]
 
-    for _ in range(args.warmup):
-        step()
+    def step(i):
+        k = i % NS
+        with torch.cuda.stream(streams[k]):
+            tr.reset_tracks(bufs[k])
+        tr.launch(tgt, dif, bufs[k], stream=streams[k], workspace=wss[k])
+
+    for i in range(args.warmup):
+        step(i)
     torch.cuda.synchronize(dev)
 
-    # timed region: barrier + sync on both sides; per-launch kernel time with events on the launch stream
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # timed region: barrier + sync on both sides
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for i in range(args.steps):
-        tr.reset_tracks(res)
-        ev[i][0].record(stream)
-        tr.launch(tgt, dif, res, stream=stream)
-        ev[i][1].record(stream)
+        step(i)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    launch_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    for k in range(1, NS):   # every batch is the same work: identical results on every stream
+        if not (torch.equal(bufs[k].converge, res.converge) and torch.equal(bufs[k].stats, res.stats)):
+            raise RuntimeError("streams disagree")
+
+    # kernel time of one launch alone (serial, HIP events on the launch stream): the
+    # roofline's denominator and the latency of one batch
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(5)]
+    for a_, b_ in ev:
+        tr.reset_tracks(res)
+        a_.record(stream)
+        tr.launch(tgt, dif, res, stream=stream)
+        b_.record(stream)
+    torch.cuda.synchronize(dev)
+    launch_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
 
     # device pose recovery + maximal support over the launch's tracks,
     # timed separately with HIP events on the same stream
@@ -223,6 +245,8 @@ def main():
             "config": {"workload": "trifocal_2op1p_30x30 config 2: 100 RANSAC samples x 312 tracks per GPU, "
                                    "Abort_RANSAC=false",
                        "samples_per_gpu": S, "tracks_per_sample": 312, "paths_per_step": paths,
+                       "streams": NS,
+                       "single_launch_paths_per_s": round(paths / (float(np.median(launch_ms)) / 1e3), 1),
                        "parallelism": f"samples sharded over {world} GPU(s), no data-path collective",
                        "GPUHC_Max_Steps": tr.settings.max_steps,
                        "GPUHC_Max_Correction_Steps": tr.settings.max_corrections,
