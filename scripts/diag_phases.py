@@ -19,7 +19,8 @@ sys.path.insert(0, ROOT)
 from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi, load_problem, load_ransac_data, prepare_target_params  # noqa
 from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker  # noqa
 
-NAMES = ["slot_phases", "park_pt", "dHdx", "dHdt_H", "lu_forward", "lu_backward", "stage_update", "lifetime", "waves"]
+NAMES = ["slot_phases", "park_pt", "dHdx", "dHdt_H", "lu_forward", "lu_backward", "stage_update", "lifetime", "waves",
+         "lu_search", "lu_bcast", "lu_rcp", "lu_update"]
 
 
 def main():
@@ -37,7 +38,7 @@ def main():
         tr.reset_tracks(r)
         tr.launch(tt, dd, r)
         torch.cuda.synchronize()
-        buf = (C.c_ulonglong * 9)()
+        buf = (C.c_ulonglong * 13)()
         fn(buf, 1)
         tr.reset_tracks(r)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -52,7 +53,7 @@ def main():
         iters = stages / 2.0   # lower bound on wave-iterations (both halves busy)
         waves = v[8]
         d = {NAMES[i]: round(v[i] / waves, 1) for i in range(8)}
-        d["per_stage_pair"] = {NAMES[i]: round(v[i] / iters, 1) for i in range(7)}
+        d["per_stage_pair"] = {NAMES[i]: round(v[i] / iters, 1) for i in list(range(7)) + list(range(9, 13))}
         d["ms"] = a.elapsed_time(b)
         d["waves"] = int(waves)
         d["stages"] = stages
