@@ -459,6 +459,42 @@ __device__ __forceinline__ int half_sum_i(int v) {
     return v;
 }
 
+// Abort-mode scoring of one half's converged path (dev-trifocal_2op1p-eval.cuh:
+// 28-250, 32 lanes per path): inlier counts of views 2 and 3 over all triplet
+// edgels.  Out of line: it runs once per converged path, and inlined its
+// registers weigh on the stage loop's allocation (72 VGPR spills).
+__device__ __attribute__((noinline)) int2 score_half(const cf *sx, const float *edgels, int num_edgels,
+                                                    const float *K, int r) {
+        Hyp hy;
+        make_hypothesis(sx, hy);
+        const float fx = K[0], fy = K[4], cx = K[3] /* eval quirk */, cy = K[5];
+        const float *R = hy.R;
+        const float d18 = hy.T[0], d19 = hy.T[1], d20 = hy.T[2], d21 = hy.T[3], d22 = hy.T[4], d23 = hy.T[5];
+        int c21 = 0, c31 = 0;
+        for (int e = r; e < num_edgels; e += 32) {
+            const float *g = edgels + (size_t)e * 6;
+            const float g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4], g5 = g[5];
+            float num, den, v0, v1, v2, ex, ey;
+            num = d20 * (R[2] * g2 + R[5] * g3 + R[8]) - (R[2] * d18 + R[5] * d19 + R[8] * d20);
+            den = 1.0f - (R[6] * g0 + R[7] * g1 + R[8]) * (R[2] * g2 + R[5] * g3 + R[8]);
+            v2 = num * (R[6] * g0 + R[7] * g1 + R[8]) + den * d20;
+            v0 = (num * (R[0] * g0 + R[1] * g1 + R[2]) + den * d18) / v2;
+            v1 = (num * (R[3] * g0 + R[4] * g1 + R[5]) + den * d19) / v2;
+            ex = (v0 * fx + cx) - (g2 * fx + cx);
+            ey = (v1 * fy + cy) - (g3 * fy + cy);
+            c21 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+            num = d23 * (R[11] * g4 + R[14] * g5 + R[17]) - (R[11] * d21 + R[14] * d22 + R[17] * d23);
+            den = 1.0f - (R[15] * g0 + R[16] * g1 + R[17]) * (R[11] * g4 + R[14] * g5 + R[17]);
+            v2 = num * (R[15] * g0 + R[16] * g1 + R[17]) + den * d23;
+            v0 = (num * (R[9] * g0 + R[10] * g1 + R[11]) + den * d21) / v2;
+            v1 = (num * (R[12] * g0 + R[13] * g1 + R[14]) + den * d22) / v2;
+            ex = (v0 * fx + cx) - (g4 * fx + cx);
+            ey = (v1 * fy + cy) - (g5 * fy + cy);
+            c31 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+        }
+        return make_int2(half_sum_i(c21), half_sum_i(c31));
+}
+
 #ifdef HC_DIAG_PHASES
 // diagnostic build: per-phase shader cycles summed over waves (k_track2):
 // [0] slot phases, [1] park + p(t), [2] dH/dx, [3] dH/dt | H, [4] LU forward,
@@ -468,8 +504,8 @@ __device__ __forceinline__ int half_sum_i(int v) {
 __device__ unsigned long long g_diag_phase[13];
 #endif
 
-template <bool ABORT, int MINW, int V>
-__global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
+template <bool ABORT, int MINW, int V, int WGT = WG_THREADS>
+__global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
     // V = 2: bpermute LU + v2 evals; V = 3: LDS-broadcast LU + packed v3 evals;
     // V = 8: v3 evals + the structurally sparse LU of hc_lu3s.hpp
     constexpr bool EV3 = V >= 3;
@@ -477,7 +513,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
                                      : (int)(sizeof(uint32_t) * (HX2_SLOT_CAP + HT_TERMS) * 32);
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
-    __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
+    __shared__ SlotLDS s_slot[2 * (WGT / WAVE)];
     TableWS *ws = a.ws;
     TableWS2 *w2 = a.ws2;
     TableWS3 *w3 = a.ws3;
@@ -488,16 +524,16 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
     uint2 *s_hx3 = reinterpret_cast<uint2 *>(s_tab);
     uint2 *s_ht3 = s_hx3 + HX3_SLOT_CAP * 32;
     if constexpr (EV3) {
-        for (int i = threadIdx.x; i < HX3_SLOT_CAP * 32; i += WG_THREADS) s_hx3[i] = w3->hx[i];   // padded table
-        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht3[i] = w3->ht[i];
+        for (int i = threadIdx.x; i < HX3_SLOT_CAP * 32; i += WGT) s_hx3[i] = w3->hx[i];   // padded table
+        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WGT) s_ht3[i] = w3->ht[i];
     } else {
-        for (int i = threadIdx.x; i < hx_len * 32; i += WG_THREADS) s_hx2[i] = w2->hx[i];
-        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) s_ht[i] = ws->ht[i];
+        for (int i = threadIdx.x; i < hx_len * 32; i += WGT) s_hx2[i] = w2->hx[i];
+        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WGT) s_ht[i] = ws->ht[i];
     }
     if (threadIdx.x < NPP) s_sp[threadIdx.x] = a.start_params[threadIdx.x];
     {
         float *z = reinterpret_cast<float *>(s_slot);
-        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
+        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WGT) z[i] = 0.0f;
     }
     __syncthreads();
     if (ABORT && threadIdx.x == 0) atomicCAS(&ws->t_start, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -548,35 +584,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track2(KArgs a) {
                     wave_lds_sync();
                     const unsigned long long im = __ballot(r >= 18 && rl && (double)__builtin_fabsf(x.y) < 1e-5);
                     if (((unsigned)(im >> hb) & 0x3FFC0000u) == 0x3FFC0000u) {   // eval.cuh:46-53
-                        Hyp hy;
-                        make_hypothesis(S.x, hy);
-                        const float fx = a.K[0], fy = a.K[4], cx = a.K[3] /* eval quirk */, cy = a.K[5];
-                        const float *R = hy.R;
-                        const float d18 = hy.T[0], d19 = hy.T[1], d20 = hy.T[2], d21 = hy.T[3], d22 = hy.T[4], d23 = hy.T[5];
-                        int c21 = 0, c31 = 0;
-                        for (int e = r; e < a.num_edgels; e += 32) {
-                            const float *g = a.edgels + (size_t)e * 6;
-                            const float g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4], g5 = g[5];
-                            float num, den, v0, v1, v2, ex, ey;
-                            num = d20 * (R[2] * g2 + R[5] * g3 + R[8]) - (R[2] * d18 + R[5] * d19 + R[8] * d20);
-                            den = 1.0f - (R[6] * g0 + R[7] * g1 + R[8]) * (R[2] * g2 + R[5] * g3 + R[8]);
-                            v2 = num * (R[6] * g0 + R[7] * g1 + R[8]) + den * d20;
-                            v0 = (num * (R[0] * g0 + R[1] * g1 + R[2]) + den * d18) / v2;
-                            v1 = (num * (R[3] * g0 + R[4] * g1 + R[5]) + den * d19) / v2;
-                            ex = (v0 * fx + cx) - (g2 * fx + cx);
-                            ey = (v1 * fy + cy) - (g3 * fy + cy);
-                            c21 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
-                            num = d23 * (R[11] * g4 + R[14] * g5 + R[17]) - (R[11] * d21 + R[14] * d22 + R[17] * d23);
-                            den = 1.0f - (R[15] * g0 + R[16] * g1 + R[17]) * (R[11] * g4 + R[14] * g5 + R[17]);
-                            v2 = num * (R[15] * g0 + R[16] * g1 + R[17]) + den * d23;
-                            v0 = (num * (R[9] * g0 + R[10] * g1 + R[11]) + den * d21) / v2;
-                            v1 = (num * (R[12] * g0 + R[13] * g1 + R[14]) + den * d22) / v2;
-                            ex = (v0 * fx + cx) - (g4 * fx + cx);
-                            ey = (v1 * fy + cy) - (g5 * fy + cy);
-                            c31 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
-                        }
-                        in21 = half_sum_i(c21);
-                        in31 = half_sum_i(c31);
+                        const int2 c = score_half(S.x, a.edgels, a.num_edgels, a.K, r);
+                        in21 = c.x;
+                        in31 = c.y;
                         const float r21 = (float)in21 / (float)a.num_edgels, r31 = (float)in31 / (float)a.num_edgels;
                         if ((double)r21 >= 0.90 && (double)r31 >= 0.90 && r == 0) {   // eval.cuh:241-246
                             __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1438,6 +1448,12 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.ws3 = ws3_of(ws);
     const int ver = kernel_version();
     const bool w4 = v3_minwaves() == 4;
+#ifdef HC_TRACK_W5
+    // experiment: 5 waves/SIMD with 640-thread workgroups (LDS: 2 per CU)
+    const bool w5 = ver == 9 && !abort_mode && getenv("HC_TRIFOCAL_OCC") && getenv("HC_TRIFOCAL_OCC")[0] == '5';
+#else
+    const bool w5 = false;
+#endif
     const void *kern = ver == 9   ? (abort_mode ? (const void *)k_track2<true, 4, 9> : (const void *)k_track2<false, 4, 9>)
                        : ver == 8 ? (abort_mode ? (const void *)k_track2<true, 4, 8> : (const void *)k_track2<false, 4, 8>)
                        : ver == 4 ? (abort_mode ? (const void *)k_track4<true> : (const void *)k_track4<false>)
@@ -1445,7 +1461,11 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
                        : ver == 2 ? (abort_mode ? (const void *)k_track2<true, 3, 2> : (const void *)k_track2<false, 3, 2>)
                        : w4       ? (abort_mode ? (const void *)k_track2<true, 4, 3> : (const void *)k_track2<false, 4, 3>)
                                   : (abort_mode ? (const void *)k_track2<true, 3, 3> : (const void *)k_track2<false, 3, 3>);
-    const int wg_threads = WG_THREADS;
+    int wg_threads = WG_THREADS;
+#ifdef HC_TRACK_W5
+    if (w5) { kern = (const void *)k_track2<false, 5, 9, 640>; wg_threads = 640; }
+#endif
+    (void)w5;
     const int grid = grid_for(ver == 4 ? (int)((paths + 3) / 4) : ver >= 2 ? (int)((paths + 1) / 2) : (int)paths,
                               kern, wg_threads);
     if (grid <= 0) return HC_ERROR_DEVICE;
