@@ -75,13 +75,13 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
     return r;
 }
 
-// Software-pipelined term loops.  Every term's table word is read up front
-// (the Jacobian registers are dead while the evaluations run), and a term's
-// operand reads are issued EV_AHEAD terms before it is computed, in program
-// order ahead of the previous terms' entry stores (which the compiler may not
-// move loads across), so a lane has several terms' LDS reads in flight instead
-// of one round trip per term.
+// Software-pipelined term loops.  A term's table word is read EV_WAHEAD terms
+// and its operands EV_AHEAD terms before it is computed, in program order
+// ahead of the previous terms' entry stores (which the compiler may not move
+// loads across), so a lane has several terms' LDS reads in flight instead of
+// one round trip per term, with few registers held.
 constexpr int EV_AHEAD = 2;
+constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
 struct HxOps { pf2 pa, pb, xu, xv; };
 __device__ __forceinline__ HxOps hx_ops(const char *sb, uint2 w) {
@@ -93,13 +93,14 @@ __device__ __forceinline__ HxOps hx_ops(const char *sb, uint2 w) {
 __device__ __forceinline__ void eval_hx3_terms(const uint2 *s_hx3, const char *sb, char *eb, int r) {
     uint2 w[HX3_SLOT_CAP];
 #pragma unroll
-    for (int k = 0; k < HX3_SLOT_CAP; k++) w[k] = s_hx3[k * 32 + r];
+    for (int k = 0; k < EV_WAHEAD; k++) w[k] = s_hx3[k * 32 + r];
     HxOps o[EV_AHEAD + 1];
 #pragma unroll
     for (int k = 0; k < EV_AHEAD; k++) o[k] = hx_ops(sb, w[k]);
     pf2 acc = {0.0f, 0.0f};
 #pragma unroll
     for (int k = 0; k < HX3_SLOT_CAP; k++) {
+        if (k + EV_WAHEAD < HX3_SLOT_CAP) w[k + EV_WAHEAD] = s_hx3[(k + EV_WAHEAD) * 32 + r];
         if (k + EV_AHEAD < HX3_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
         const HxOps &q = o[k % (EV_AHEAD + 1)];
         const float co = (float)(int)(int8_t)(uint8_t)(w[k].y >> 16);
@@ -124,11 +125,17 @@ __device__ __forceinline__ void eval_hx3(cf (&rA)[NV], const uint2 *s_hx3, int h
     (void)hx_len;
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
     eval_hx3_terms(s_hx3, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
-    if (r < NV) ent_row[6] = cmk(0.0f, 0.0f);   // structural zero (the v3 LU reuses this block)
+    float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    if (r < NV) ent_row[6] = cmk(z, z);   // structural zero (the v3 LU reuses this block)
     wave_lds_sync();
+    // opaque copy: keeps LICM from hoisting the 30 decoded gather addresses out
+    // of the path loop (30 VGPRs held across the LU, then spilled)
+    uint32_t m[3] = {map[0], map[1], map[2]};
+    asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]));
 #pragma unroll
     for (int c = 0; c < NV; c++) {
-        const uint32_t code = (map[c / 10] >> (3 * (c % 10))) & 7u;
+        const uint32_t code = (m[c / 10] >> (3 * (c % 10))) & 7u;
         rA[c] = ent_row[code];
     }
 }
@@ -145,13 +152,14 @@ __device__ __forceinline__ cf eval_ht3(const uint2 *s_ht3, const SlotLDS &S, int
     const char *sb = reinterpret_cast<const char *>(&S);
     uint2 w[HT_TERMS];
 #pragma unroll
-    for (int j = 0; j < HT_TERMS; j++) w[j] = s_ht3[j * 32 + r];
+    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht3[j * 32 + r];
     HtOps o[EV_AHEAD + 1];
 #pragma unroll
     for (int j = 0; j < EV_AHEAD; j++) o[j] = ht_ops(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < HT_TERMS; j++) {
+        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht3[(j + EV_WAHEAD) * 32 + r];
         if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = ht_ops(sb, w[j + EV_AHEAD]);
         const HtOps &q = o[j % (EV_AHEAD + 1)];
         const float co = (float)((int)w[j].y >> 24);
@@ -174,13 +182,14 @@ __device__ __forceinline__ cf eval_h3(const uint2 *s_ht3, const SlotLDS &S, int 
     const char *sb = reinterpret_cast<const char *>(&S);
     uint2 w[HT_TERMS];
 #pragma unroll
-    for (int j = 0; j < HT_TERMS; j++) w[j] = s_ht3[j * 32 + r];
+    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht3[j * 32 + r];
     HOps o[EV_AHEAD + 1];
 #pragma unroll
     for (int j = 0; j < EV_AHEAD; j++) o[j] = h_ops(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < HT_TERMS; j++) {
+        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht3[(j + EV_WAHEAD) * 32 + r];
         if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = h_ops(sb, w[j + EV_AHEAD]);
         const HOps &q = o[j % (EV_AHEAD + 1)];
         const float co = (float)((int)w[j].y >> 24);

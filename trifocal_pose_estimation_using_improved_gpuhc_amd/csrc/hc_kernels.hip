@@ -463,36 +463,44 @@ __device__ __forceinline__ int half_sum_i(int v) {
 // 28-250, 32 lanes per path): inlier counts of views 2 and 3 over all triplet
 // edgels.  Out of line: it runs once per converged path, and inlined its
 // registers weigh on the stage loop's allocation (72 VGPR spills).
-__device__ __attribute__((noinline)) int2 score_half(const cf *sx, const float *edgels, int num_edgels,
-                                                    const float *K, int r) {
+template <int VIEW>   // 0: view 2 (edgel columns 2, 3), 1: view 3 (columns 4, 5)
+__device__ __forceinline__ int score_view(const float *R, float da, float db, float dc, const float *edgels,
+                                          int num_edgels, float fx, float fy, float cx, float cy, int r) {
+    int c = 0;
+    for (int e = r; e < num_edgels; e += 32) {
+        const float *g = edgels + (size_t)e * 6;
+        const float g0 = g[0], g1 = g[1], gu = g[2 + 2 * VIEW], gv = g[3 + 2 * VIEW];
+        const float num = dc * (R[2] * gu + R[5] * gv + R[8]) - (R[2] * da + R[5] * db + R[8] * dc);
+        const float den = 1.0f - (R[6] * g0 + R[7] * g1 + R[8]) * (R[2] * gu + R[5] * gv + R[8]);
+        const float v2 = num * (R[6] * g0 + R[7] * g1 + R[8]) + den * dc;
+        const float v0 = (num * (R[0] * g0 + R[1] * g1 + R[2]) + den * da) / v2;
+        const float v1 = (num * (R[3] * g0 + R[4] * g1 + R[5]) + den * db) / v2;
+        const float ex = (v0 * fx + cx) - (gu * fx + cx);
+        const float ey = (v1 * fy + cy) - (gv * fy + cy);
+        c += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
+    }
+    return c;
+}
+// The two views are scored in separate passes, each from its own evaluation
+// of the hypothesis (12 live values instead of 24): the abort kernel's register
+// allocation is otherwise set by this cold path.
+__device__ __forceinline__ int2 score_half(const cf *sx, const float *edgels, int num_edgels,
+                                           const float *K, int r) {
+    const float fx = K[0], fy = K[4], cx = K[3] /* eval quirk */, cy = K[5];
+    int c21, c31;
+    {
         Hyp hy;
         make_hypothesis(sx, hy);
-        const float fx = K[0], fy = K[4], cx = K[3] /* eval quirk */, cy = K[5];
-        const float *R = hy.R;
-        const float d18 = hy.T[0], d19 = hy.T[1], d20 = hy.T[2], d21 = hy.T[3], d22 = hy.T[4], d23 = hy.T[5];
-        int c21 = 0, c31 = 0;
-        for (int e = r; e < num_edgels; e += 32) {
-            const float *g = edgels + (size_t)e * 6;
-            const float g0 = g[0], g1 = g[1], g2 = g[2], g3 = g[3], g4 = g[4], g5 = g[5];
-            float num, den, v0, v1, v2, ex, ey;
-            num = d20 * (R[2] * g2 + R[5] * g3 + R[8]) - (R[2] * d18 + R[5] * d19 + R[8] * d20);
-            den = 1.0f - (R[6] * g0 + R[7] * g1 + R[8]) * (R[2] * g2 + R[5] * g3 + R[8]);
-            v2 = num * (R[6] * g0 + R[7] * g1 + R[8]) + den * d20;
-            v0 = (num * (R[0] * g0 + R[1] * g1 + R[2]) + den * d18) / v2;
-            v1 = (num * (R[3] * g0 + R[4] * g1 + R[5]) + den * d19) / v2;
-            ex = (v0 * fx + cx) - (g2 * fx + cx);
-            ey = (v1 * fy + cy) - (g3 * fy + cy);
-            c21 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
-            num = d23 * (R[11] * g4 + R[14] * g5 + R[17]) - (R[11] * d21 + R[14] * d22 + R[17] * d23);
-            den = 1.0f - (R[15] * g0 + R[16] * g1 + R[17]) * (R[11] * g4 + R[14] * g5 + R[17]);
-            v2 = num * (R[15] * g0 + R[16] * g1 + R[17]) + den * d23;
-            v0 = (num * (R[9] * g0 + R[10] * g1 + R[11]) + den * d21) / v2;
-            v1 = (num * (R[12] * g0 + R[13] * g1 + R[14]) + den * d22) / v2;
-            ex = (v0 * fx + cx) - (g4 * fx + cx);
-            ey = (v1 * fy + cy) - (g5 * fy + cy);
-            c31 += (__builtin_sqrtf(ex * ex + ey * ey) < 2.0f) ? 1 : 0;
-        }
-        return make_int2(half_sum_i(c21), half_sum_i(c31));
+        c21 = score_view<0>(hy.R, hy.T[0], hy.T[1], hy.T[2], edgels, num_edgels, fx, fy, cx, cy, r);
+    }
+    {
+        const cf *sx2 = sx;
+        asm volatile("" : "+v"(sx2));   // a second evaluation, not the first one kept live
+        Hyp hy;
+        make_hypothesis(sx2, hy);
+        c31 = score_view<1>(hy.R + 9, hy.T[3], hy.T[4], hy.T[5], edgels, num_edgels, fx, fy, cx, cy, r);
+    }
+    return make_int2(half_sum_i(c21), half_sum_i(c31));
 }
 
 #ifdef HC_DIAG_PHASES
@@ -543,13 +551,23 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
     SlotLDS &S = s_slot[wid * 2 + (hb >> 5)];
     if (r == 30) S.x[30] = cmk(1.0f, 0.0f);
     if (r == 0) S.p[33] = cmk(1.0f, 0.0f);
-    const uint32_t map[3] = {w2->map[0][r], w2->map[1][r], w2->map[2][r]};
-    const uint32_t row_pat = V >= 8 ? row_pattern(map) : 0u;   // structural pattern of row r (v8 LU)
+    // per-row constants (column->slot maps, structural pattern) live in LDS and
+    // are re-read every stage: held in VGPRs across the loop they spill (abort mode)
+    __shared__ uint32_t s_rowc[4][32];
+    if (threadIdx.x < 32) {
+        const uint32_t m0[3] = {w2->map[0][threadIdx.x], w2->map[1][threadIdx.x], w2->map[2][threadIdx.x]};
+        s_rowc[0][threadIdx.x] = m0[0];
+        s_rowc[1][threadIdx.x] = m0[1];
+        s_rowc[2][threadIdx.x] = m0[2];
+        s_rowc[3][threadIdx.x] = V >= 8 ? row_pattern(m0) : 0u;   // structural pattern of row r (v8 LU)
+    }
+    __syncthreads();
     const bool rl = r < NV;
     wave_lds_sync();
 
     // per-slot state (uniform within a half)
     int ph = PH_DEQ, b = -1, smp_loaded = -1;
+    unsigned found_seen = 0u;   // abort mode: the found flag as of the last stage
 #ifdef HC_DIAG_TIMES
     int diag_t0 = 0;
 #endif
@@ -654,6 +672,18 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
                     }
                 }
             }
+            if (ABORT && ph == PH_BEGIN && stepidx > 0 && found_seen != 0u) {
+                // a pose was found: a path in flight stops at its step boundary and
+                // reports like a skipped one (track untouched, conv = 0).  The
+                // reference's in-flight blocks run on (..._TrunRANSAC.cu:152 only
+                // gates the start); their results are not read once found.
+                if (r == 0) {
+                    a.conv[b] = 0;
+                    a.inf[b] = 0;
+                    if (a.stats) a.stats[b] = hcPathStats{0, 0, 0, 0};
+                }
+                ph = PH_DEQ;
+            }
             if (ph == PH_BEGIN) {                                             // :138-165
                 bool done = stepidx > a.max_steps;
                 if (!done) done = !((double)t0 < 1.0 && (1.0 - (double)t0 > 0.0000001));
@@ -685,6 +715,10 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
         }
         if (__ballot(ph == PH_STAGE) == 0ull) break;
         HC_DIAG_MARK(0);
+        // the found flag for the next step boundary: read now, used after the stage
+#ifndef HC_NO_INFLIGHT_STOP
+        if (ABORT) found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 
         // ---------------- one stage for both slots
         // park the slot state in LDS so it does not occupy VGPRs across eval + LU
@@ -703,7 +737,9 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
             const bool pred0 = act0 && s < 4;
             if (pred0 && r < NPP - 1) {                                      // :181 p(t), i < 33
                 const float omt = (float)(1.0 - (double)t0);
-                S.p[r] = cadd(cscale(S.tgt[r], t0), cscale(s_sp[r], omt));
+                const cf *sp = s_sp;   // opaque base: the address is not hoisted and held across the loop
+                asm volatile("" : "+v"(sp));
+                S.p[r] = cadd(cscale(S.tgt[r], t0), cscale(sp[r], omt));
             }
             if (pred0 && r == 0) S.p[32] = cadd(cscale(S.tgt[32], t0), cscale(s_sp[32], (float)(1.0 - (double)t0)));
         }
@@ -712,9 +748,11 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
         asm volatile("" :: "v"(s_in), "v"(ph_in));
         // opaque lane id: keeps LICM from hoisting ~30 lane-derived per-pivot
         // constants (bpermute addresses, r == i masks) out of the path loop
-        int lane_v = lane;
+        int lane_v = lane_id();   // recomputed (2 VALU), not held across the loop
         asm volatile("" : "+v"(lane_v));
         const int r_v = lane_v & 31;
+        const uint32_t map[3] = {s_rowc[0][r_v], s_rowc[1][r_v], s_rowc[2][r_v]};
+        const uint32_t row_pat = s_rowc[3][r_v];
         const bool act = ph_in == PH_STAGE;
         const bool pred = act && s_in < 4;
         HC_DIAG_MARK(1);

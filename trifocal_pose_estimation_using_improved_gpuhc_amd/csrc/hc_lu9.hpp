@@ -25,11 +25,28 @@
 
 namespace hc {
 
-enum : int { LU9_SPEC = 1, LU9_NOMASK = 2, LU9_PF = 4, LU9_BRL = 8, LU9_LEAN = 16, LU9_BOUT = 32, LU9_ONEB = 1024,
+enum : int { LU9_SPEC = 1, LU9_NOMASK = 2, LU9_PF = 4, LU9_BRL = 8, LU9_LEAN = 16, LU9_BOUT = 32, LU9_ONEB = 1024, LU9_RCPA = 2048, LU9_BSPLIT = 4096,
              // timing-only ablations for scripts/lu_lab.hip (results wrong)
              LU9_X_NOUPD = 64, LU9_X_NOBACK = 128, LU9_X_NOSEARCH = 256, LU9_X_NOBCAST = 512 };
 // the tracker's configuration (scripts/lu_lab.hip: fastest bit-identical combination)
-constexpr int LU9_PROD = LU9_BRL | LU9_LEAN | LU9_ONEB;
+constexpr int LU9_PROD = LU9_BRL | LU9_LEAN | LU9_ONEB | LU9_RCPA;
+
+
+// cuCdivf(1, y) for s = |y.re| + |y.im| in the fast range, in packed FP32 with
+// the spec's ops (cdiv_factors_fast + the quotient of DESIGN.md §4):
+// o1 = 1/s, (brs, bis) = y*o1, o2 = 1/(brs*brs + bis*bis),
+// 1/y = ((o1*brs)*o2, (-(o1*bis))*o2); -(o1*bis) is computed as o1*(-bis)
+// (IEEE: the same value).  oo returns (o1, o2).
+__device__ __forceinline__ pf2 recip_fast(pf2 y, float s, pf2 &oo) {
+    oo.x = rcp_rn(s);
+    pf2 bb, sq, q, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(bb) : "v"(y), "v"(oo));
+    asm("v_pk_mul_f32 %0, %1, %1" : "=v"(sq) : "v"(bb));
+    oo.y = rcp_rn(sq.x + sq.y);
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(q) : "v"(oo), "v"(bb));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(q), "v"(oo));
+    return r;
+}
 
 // column chunks of the update of step I: a leading single column when I+1 is
 // odd, then groups of CH (even) columns
@@ -218,8 +235,16 @@ __device__ __forceinline__ void lu9_forward(cf (&rA)[NV], cf &rB, int &rowid, ui
             reg = sxi;
         } else {
             if (__builtin_expect(!dense, 1)) {
-                f = cdiv_factors_fast(sxi, piv_abs);
-                reg = cmk((f.o1 * f.brs) * f.o2, (-(f.o1 * f.bis)) * f.o2);
+                if constexpr (F & LU9_RCPA) {
+                    pf2 oo;
+                    const pf2 rg = recip_fast(pf2{sxi.x, sxi.y}, piv_abs, oo);
+                    reg = cmk(rg.x, rg.y);
+                    f.o1 = oo.x;
+                    f.o2 = oo.y;
+                } else {
+                    f = cdiv_factors_fast(sxi, piv_abs);
+                    reg = cmk((f.o1 * f.brs) * f.o2, (-(f.o1 * f.bis)) * f.o2);
+                }
             } else {
                 f = cdiv_factors(sxi);
                 reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
@@ -265,7 +290,7 @@ __device__ __forceinline__ void lu9_forward(cf (&rA)[NV], cf &rB, int &rowid, ui
 
 // back substitution, x_I broadcast with v_readlane from the owner lane of each
 // half (found by a ballot on the final row ids)
-template <int I>
+template <int I, bool SPLIT>
 __device__ __forceinline__ void lu9_backward_rl(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, int hb) {
     if constexpr (I >= 0) {
         const unsigned long long own = __builtin_amdgcn_ballot_w64(rowid == I);
@@ -276,13 +301,33 @@ __device__ __forceinline__ void lu9_backward_rl(const cf (&rA)[NV], cf &rB, int 
         const float y0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o0));
         const float x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.x), o1));
         const float y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o1));
+        if constexpr (SPLIT) {
+            // each half subtracts its own owner's x_I, an SGPR pair operand
+            const bool own_lane = rowid == I;
+            if (rowid < I) {
+                const pf2 a = pf2{rA[I].x, rA[I].y};
+                pf2 v = pf2{rB.x, rB.y}, t;
+                if (hb == 0) {
+                    const pf2 xs = pf2{x0, y0};
+                    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(t) : "s"(xs), "v"(a), "v"(v));
+                    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]" : "=v"(v) : "s"(xs), "v"(a), "v"(t));
+                } else {
+                    const pf2 xs = pf2{x1, y1};
+                    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]" : "=v"(t) : "s"(xs), "v"(a), "v"(v));
+                    asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]" : "=v"(v) : "s"(xs), "v"(a), "v"(t));
+                }
+                rB = cmk(v.x, v.y);
+            }
+            if (own_lane) rB = cmk(q.x, q.y);   // the owner keeps its x_I (returned below)
+        } else {
         const cf xi = hb ? cmk(x1, y1) : cmk(x0, y0);
         if (rowid < I) {
             const pf2 v = pcmsub(pf2{rB.x, rB.y}, pf2{xi.x, xi.y}, pf2{rA[I].x, rA[I].y});
             rB = cmk(v.x, v.y);
         }
         if (rowid == I) rB = xi;   // the owner keeps its x_I (returned below)
-        lu9_backward_rl<I - 1>(rA, rB, rowid, my, hb);
+        }
+        lu9_backward_rl<I - 1, SPLIT>(rA, rB, rowid, my, hb);
     }
 }
 
@@ -303,7 +348,7 @@ __device__ __forceinline__ cf lu_solve9(cf (&rA)[NV], cf rB, int lane, uint32_t 
         wave_lds_sync();
         return L.row[row_lane ? r : 0];
     } else if constexpr (F & LU9_BRL) {
-        lu9_backward_rl<NV - 1>(rA, rB, rowid, my, hb);
+        lu9_backward_rl<NV - 1, (F & LU9_BSPLIT) != 0>(rA, rB, rowid, my, hb);
         // lane r returns x_r: the owner of position r holds it in rB
         const unsigned long long dummy = 0;
         (void)dummy;
