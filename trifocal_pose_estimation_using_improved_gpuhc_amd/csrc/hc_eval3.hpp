@@ -80,7 +80,10 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
 // ahead of the previous terms' entry stores (which the compiler may not move
 // loads across), so a lane has several terms' LDS reads in flight instead of
 // one round trip per term, with few registers held.
-constexpr int EV_AHEAD = 2;
+#ifndef HC_EV_AHEAD
+#define HC_EV_AHEAD 2
+#endif
+constexpr int EV_AHEAD = HC_EV_AHEAD;
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
 struct HxOps { pf2 pa, pb, xu, xv; };
