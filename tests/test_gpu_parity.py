@@ -88,6 +88,41 @@ def test_cgesv_edge_cases(oracle):
     assert np.median(res) < 1e-4
 
 
+def test_cgesv_extreme_scales(problem, oracle, samples100):
+    """Every exit of the v9 LU's fast pivot step (hc_lu9.hpp): pivots below 2^-90
+    and at/above 2^120, entries at/above 2^88 (the whole solve runs dense), an
+    infinity, NaN at the pivot position, denormals, and structurally sparse
+    tracker Jacobians at those scales -- bit-exact against the oracle."""
+    from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import cgesv_batched
+    tgt, dif, _ = samples100
+    X, P, D = _jacobians_from_path(problem, oracle, tgt, dif, n=8, seed=5)
+    J = np.stack([oracle.eval_hx(problem.dHdx_index, X[i], P[i]) for i in range(8)])
+    bJ = np.stack([oracle.eval_ht(problem.dHdt_index, X[i], P[i], D[i]) for i in range(8)])
+    rng = np.random.default_rng(12)
+    As, bs = [], []
+    for scale in (2.0 ** -100, 2.0 ** -60, 2.0 ** 60, 2.0 ** 90, 2.0 ** 121):
+        for i in range(4):
+            As.append((J[i] * np.float32(scale)).astype(np.float32))
+            bs.append(bJ[i])
+    A = rng.standard_normal((6, 30, 30, 2)).astype(np.float32)
+    A[0, 4, 4, :] = np.float32(2.0 ** -95)        # tiny diagonal, large elsewhere in column
+    A[0, :, 4, :] *= np.float32(2.0 ** -100)      # whole column tiny -> tiny pivot
+    A[1, 2, 7, 0] = np.inf                        # an infinity
+    A[2, :, :, :] = np.diag(np.full(30, np.nan, np.float32))[..., None]   # NaN on the diagonal...
+    A[2, :, :, :] += rng.standard_normal((30, 30, 2)).astype(np.float32)  # ...plus finite noise
+    A[3, :, :, :] *= np.float32(1e-40)            # denormals
+    A[4, 9, 9, :] = np.float32(2.0 ** 125)        # one huge entry
+    A[5, :, 0, :] = 0.0
+    A[5, 3, 0, :] = np.float32(2.0 ** -126)       # smallest normal as the only pivot candidate
+    As.extend(A)
+    bs.extend(rng.standard_normal((6, 30, 2)).astype(np.float32))
+    As, bs = np.stack(As), np.stack(bs)
+    xg = cgesv_batched(As, bs)
+    for i in range(As.shape[0]):
+        xr = oracle.cgesv_gpu(As[i], bs[i])
+        assert same(xg[i], xr).all(), f"extreme-scale LU mismatch on system {i}"
+
+
 def test_tracker_matches_oracle_small(problem, oracle, samples100, tracker):
     """Full GPU-HC tracking of 2 samples (624 paths) vs the oracle, value for value."""
     tgt, dif, _ = samples100
