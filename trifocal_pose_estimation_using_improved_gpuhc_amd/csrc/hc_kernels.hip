@@ -866,7 +866,10 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
 // predictor or corrector stage (p(t), dH/dx, dH/dt|H, LU) for all four slots.
 // The stage logic is k_track2's (..._TrunPaths.cu:138-280) per row.
 template <bool ABORT>
-__global__ void __launch_bounds__(WG_THREADS, 2) k_track4(KArgs a) {
+#ifndef HC_V4_MINW
+#define HC_V4_MINW 2
+#endif
+__global__ void __launch_bounds__(WG_THREADS, HC_V4_MINW) k_track4(KArgs a) {
     constexpr int TAB_BYTES = (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32);
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
