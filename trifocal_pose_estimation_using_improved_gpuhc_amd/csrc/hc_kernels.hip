@@ -1615,7 +1615,7 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
         hipLaunchKernelGGL(hc::k_eval4, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
                            (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
                            (hc::cf *)H);
-    } else if (hc::kernel_version() == 3 || hc::kernel_version() == 8) {
+    } else if (hc::kernel_version() == 3 || hc::kernel_version() >= 8) {
         const int per = 2 * hc::WAVES_PER_WG;
         hipLaunchKernelGGL(hc::k_eval3, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
                            (const hc::cf *)x, (const hc::cf *)p, (const hc::cf *)d, (hc::cf *)Hx, (hc::cf *)Ht,
