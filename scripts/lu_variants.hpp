@@ -9,4 +9,4 @@ __device__ __forceinline__ cf lab_variant(cf (&rA)[NV], cf rB, int lane, uint32_
     else return lu_solve9<V - 1000>(rA, rB, lane, pat, L);
 }
 }  // namespace hc
-#define LU_LAB_RUNS run<2048>(d, reps, &ref, o);
+#define LU_LAB_RUNS run<4096>(d, reps, &ref, o); run<12288>(d, reps, &ref, o); run<4096>(d, reps, &ref, o); run<12288>(d, reps, &ref, o);

@@ -25,7 +25,7 @@
 
 namespace hc {
 
-enum : int { LU9_SPEC = 1, LU9_NOMASK = 2, LU9_PF = 4, LU9_BRL = 8, LU9_LEAN = 16, LU9_BOUT = 32, LU9_ONEB = 1024, LU9_RCPA = 2048, LU9_BSPLIT = 4096,
+enum : int { LU9_SPEC = 1, LU9_NOMASK = 2, LU9_PF = 4, LU9_BRL = 8, LU9_LEAN = 16, LU9_BOUT = 32, LU9_ONEB = 1024, LU9_RCPA = 2048, LU9_BSPLIT = 4096, LU9_EARLY = 8192,
              // timing-only ablations for scripts/lu_lab.hip (results wrong)
              LU9_X_NOUPD = 64, LU9_X_NOBACK = 128, LU9_X_NOSEARCH = 256, LU9_X_NOBCAST = 512 };
 // the tracker's configuration (scripts/lu_lab.hip: fastest bit-identical combination)
@@ -100,7 +100,7 @@ __device__ __forceinline__ void lu9_update(cf (&rA)[NV], const cf &l, bool below
             if constexpr (K + 1 < C::count(I)) {
                 if (pmw & C::mask(I, K + 1)) lu9_load<CH, I, K + 1>(B, L);
             }
-        } else {
+        } else if constexpr (!((F & LU9_EARLY) && K == 0)) {
             if (pmw & C::mask(I, K)) lu9_load<CH, I, K>(B, L);
         }
         if (pmw & C::mask(I, K)) {
@@ -224,7 +224,7 @@ __device__ __forceinline__ void lu9_forward(cf (&rA)[NV], cf &rB, int &rowid, ui
         if constexpr (F & LU9_SPEC) asm volatile("" : "+v"(my.oo));
         wave_lds_sync();
         Lu9Buf<LU3S_CHUNK> B;
-        if constexpr ((F & LU9_PF) && Lu9Chunks<LU3S_CHUNK>::count(I) > 0) {
+        if constexpr ((F & (LU9_PF | LU9_EARLY)) && Lu9Chunks<LU3S_CHUNK>::count(I) > 0) {
             if (pmw & Lu9Chunks<LU3S_CHUNK>::mask(I, 0)) lu9_load<LU3S_CHUNK, I, 0>(B, L);
         }
         const cf sxi = L.row[I];
