@@ -512,12 +512,14 @@ __device__ __forceinline__ int2 score_half(const cf *sx, const float *edgels, in
 __device__ unsigned long long g_diag_phase[13];
 #endif
 
-template <bool ABORT, int MINW, int V, int WGT = WG_THREADS>
+// GTAB: the term tables are read from the workspace (global, L1/L2-resident)
+// instead of being staged in LDS (10 KB less LDS per workgroup; experiment)
+template <bool ABORT, int MINW, int V, int WGT = WG_THREADS, bool GTAB = false>
 __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
     // V = 2: bpermute LU + v2 evals; V = 3: LDS-broadcast LU + packed v3 evals;
     // V = 8: v3 evals + the structurally sparse LU of hc_lu3s.hpp
     constexpr bool EV3 = V >= 3;
-    constexpr int TAB_BYTES = EV3 ? (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32)
+    constexpr int TAB_BYTES = GTAB ? 16 : EV3 ? (int)(sizeof(uint2) * (HX3_SLOT_CAP + HT_TERMS) * 32)
                                      : (int)(sizeof(uint32_t) * (HX2_SLOT_CAP + HT_TERMS) * 32);
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
@@ -529,11 +531,13 @@ __global__ void __launch_bounds__(WGT, MINW) k_track2(KArgs a) {
     const int hx_len = EV3 ? w3->hx_len : w2->hx_len;
     uint32_t *s_hx2 = reinterpret_cast<uint32_t *>(s_tab);
     uint32_t *s_ht = s_hx2 + HX2_SLOT_CAP * 32;
-    uint2 *s_hx3 = reinterpret_cast<uint2 *>(s_tab);
-    uint2 *s_ht3 = s_hx3 + HX3_SLOT_CAP * 32;
-    if constexpr (EV3) {
-        for (int i = threadIdx.x; i < HX3_SLOT_CAP * 32; i += WGT) s_hx3[i] = w3->hx[i];   // padded table
-        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WGT) s_ht3[i] = w3->ht[i];
+    const uint2 *s_hx3 = GTAB ? w3->hx : reinterpret_cast<const uint2 *>(s_tab);
+    const uint2 *s_ht3 = GTAB ? w3->ht : reinterpret_cast<const uint2 *>(s_tab) + HX3_SLOT_CAP * 32;
+    if constexpr (GTAB) {
+    } else if constexpr (EV3) {
+        uint2 *t_hx3 = reinterpret_cast<uint2 *>(s_tab), *t_ht3 = t_hx3 + HX3_SLOT_CAP * 32;
+        for (int i = threadIdx.x; i < HX3_SLOT_CAP * 32; i += WGT) t_hx3[i] = w3->hx[i];   // padded table
+        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WGT) t_ht3[i] = w3->ht[i];
     } else {
         for (int i = threadIdx.x; i < hx_len * 32; i += WGT) s_hx2[i] = w2->hx[i];
         for (int i = threadIdx.x; i < HT_TERMS * 32; i += WGT) s_ht[i] = ws->ht[i];
@@ -1389,6 +1393,14 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval4(int n, TableWS *ws, const 
 // baselines, all bit-identical); default v9 = v3 evals + the structurally
 // sparse LU with lean pivot steps (hc_lu9.hpp); v8 = the sparse LU of
 // hc_lu3s.hpp.  v4: four paths per wave (hc_track4.hpp).
+static int v9_waves() {
+    static int w = -1;
+    if (w < 0) {
+        const char *e = getenv("HC_TRIFOCAL_V9_WAVES");
+        w = (e && e[0] == '4') ? 4 : 5;
+    }
+    return w;
+}
 static int kernel_version() {
     static int v = -1;
     if (v < 0) {
@@ -1442,7 +1454,12 @@ static int grid_for(int waves_needed, const void *kernel, int wg_threads = WG_TH
     }
     const int wpg = wg_threads / WAVE;
     const int want = (waves_needed + wpg - 1) / wpg;
-    const int cap = cache_cus * cache_blocks;
+    int per_cu = cache_blocks;
+    // HC_TRIFOCAL_WGS_PER_CU: fewer resident workgroups per CU than the occupancy
+    // limit (experiment: fewer path slots, more paths per slot)
+    static const char *cap_env = getenv("HC_TRIFOCAL_WGS_PER_CU");
+    if (cap_env && atoi(cap_env) > 0 && atoi(cap_env) < per_cu) per_cu = atoi(cap_env);
+    const int cap = cache_cus * per_cu;
     return want < cap ? want : cap;
 }
 
@@ -1506,6 +1523,10 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
 #ifdef HC_TRACK_W5
     if (w5) { kern = (const void *)k_track2<false, 5, 9, 640>; wg_threads = 640; }
 #endif
+    // v9 tracking (abort off): term tables read from the workspace (L1/L2) instead of
+    // LDS, which leaves 27.5 KB LDS and 96 VGPRs per 4-wave workgroup: 5 waves/SIMD.
+    // HC_TRIFOCAL_V9_WAVES=4 selects the 4-wave kernel with LDS-staged tables.
+    if (ver == 9 && !abort_mode && v9_waves() == 5) kern = (const void *)k_track2<false, 5, 9, 256, true>;
     (void)w5;
     const int grid = grid_for(ver == 4 ? (int)((paths + 3) / 4) : ver >= 2 ? (int)((paths + 1) / 2) : (int)paths,
                               kern, wg_threads);
@@ -1639,7 +1660,8 @@ const char *hc_trifocal_version(void) {
     switch (hc::kernel_version()) {
     case 1: return "hc_trifocal gfx950 v1 (wave-per-path, register LU)";
     case 2: return "hc_trifocal gfx950 v2 (2 paths/wave, bpermute LU, per-lane term lists)";
-    case 9: return "hc_trifocal gfx950 v9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and readlane back substitution, pipelined evals, 4 waves/SIMD)";
+    case 9: return hc::v9_waves() == 5 ? "hc_trifocal gfx950 v9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and readlane back substitution, pipelined evals, 5 waves/SIMD)"
+                                   : "hc_trifocal gfx950 v9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and readlane back substitution, pipelined evals, 4 waves/SIMD)";
     case 8: return "hc_trifocal gfx950 v8 (2 paths/wave, structurally sparse LDS-broadcast LU, packed evals, 4 waves/SIMD)";
     case 4: return "hc_trifocal gfx950 v4 (4 paths/wave, 2 rows/lane, LDS-broadcast LU, packed evals, 2 waves/SIMD)";
     default:
