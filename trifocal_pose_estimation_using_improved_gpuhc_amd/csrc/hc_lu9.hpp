@@ -32,7 +32,10 @@ enum : int { LU9_SPEC = 1, LU9_NOMASK = 2, LU9_PF = 4, LU9_BRL = 8, LU9_LEAN = 1
 #ifndef HC_LU9_EXTRA
 #define HC_LU9_EXTRA 0
 #endif
-constexpr int LU9_PROD = LU9_BRL | LU9_LEAN | LU9_ONEB | LU9_RCPA | HC_LU9_EXTRA;
+#ifndef HC_LU9_DROP
+#define HC_LU9_DROP 0
+#endif
+constexpr int LU9_PROD = ((LU9_BRL | LU9_LEAN | LU9_ONEB | LU9_RCPA) & ~HC_LU9_DROP) | HC_LU9_EXTRA;
 
 
 // cuCdivf(1, y) for s = |y.re| + |y.im| in the fast range, in packed FP32 with
