@@ -57,7 +57,7 @@ def parse():
     ap.add_argument("--noisy-trials", type=int, default=10,
                     help="config 5: RANSAC runs on sigma=1px noisy synthcurves (pose success rate); 0 disables")
     ap.add_argument("--noisy-sigma", type=float, default=1.0)
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=4,
                     help="HIP streams the timed steps rotate over: step i runs on stream i %% streams with its own "
                          "track buffers and workspace, so one batch's tail overlaps the next batch's start "
                          "(1 = strictly serial launches)")
