@@ -101,6 +101,7 @@ private:
     int GPUHC_Max_Steps = 80, GPUHC_Max_Correction_Steps = 3, GPUHC_delta_t_incremental_steps = 4;
     int Num_Of_Vars = 30, Num_Of_Params = 33, Num_Of_Tracks = 312;
     bool Abort_RANSAC_by_Good_Sol = false;
+    bool Abort_Inflight_Stop = false;   // not in the reference: hcAbortArgs::inflight_stop
     int Pose_Flags = 0;   // Pose_Selection_Reference_Quirks -> HC_POSE_REFERENCE_QUIRKS
     int Num_Of_GPUs = 1;
     int Num_Of_RANSAC_Iterations = 100;   // NUM_OF_RANSAC_ITERATIONS (definitions.hpp:12), runtime here

@@ -102,6 +102,13 @@ typedef struct {
     const float *intrinsic_matrix;        /* 9 floats, row-major K               */
     uint8_t *found_trifocal_sols;         /* 1 byte flag (caller zeroes it)      */
     int32_t *trifocal_sols_batch_index;   /* 312*N ints (caller sets -1)         */
+    /* 0 (default, the reference's semantics, ..._TrunRANSAC.cu:148-152): the
+       flag only gates a path's start; paths already in flight when a good
+       hypothesis is found run to completion and write their results.
+       1: paths in flight also stop at their next step boundary and report
+       like a skipped path (track untouched, converge = 0) -- a faster kernel
+       exit, same time to the first good pose. */
+    int inflight_stop;
 } hcAbortArgs;
 
 /* Workspace: holds the compacted index tables, the path work queue and the
@@ -119,8 +126,14 @@ hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAb
                                              void *workspace, size_t workspace_bytes,
                                              hcStream stream);
 
+/* HC_SUCCESS, or HC_ERROR_TABLE when the last launch on this workspace found
+   an index table that does not fit the kernels' compaction (the tracker then
+   left every output untouched).  Blocking read -- call after synchronising. */
+hcStatus hc_trifocal_workspace_status(const void *workspace);
+
 /* Device timestamps of the last launch on this workspace, in seconds since the
    launch started: [0] = first good hypothesis found (abort mode, <0 if none).
+   The device clock rate is queried (hipDeviceAttributeWallClockRate).
    Reads the workspace with a blocking copy -- call after synchronising. */
 hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_seconds);
 

@@ -1,4 +1,4 @@
-# usage: bash scripts/profile.sh TAG   (env HC_TRIFOCAL_* passes through)
+# usage: bash scripts/profile.sh TAG
 # kernel trace + stats, then one PMC pass per counter group (never combined with traces)
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp

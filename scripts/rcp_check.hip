@@ -1,6 +1,6 @@
 // Exhaustive check of reciprocal sequences against IEEE 1.0f/s on the GPU,
 // for every float s = m * 2^e with m in [1,2) (all 2^23 significands) and
-// e in [-90, 119] -- the fast-path range of hc_lu3.hpp's rcp_rn.
+// e in [-90, 119] -- the fast-path range of hc_lu.hpp's rcp_rn.
 //   A: rcp + 2 fma (one Newton step)        B: A + 2 fma        C: B + 2 fma (= hipcc's div core)
 // Output: one JSON line with mismatch counts.  Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off
 #include <hip/hip_runtime.h>

@@ -89,7 +89,7 @@ def test_cgesv_edge_cases(oracle):
 
 
 def test_cgesv_extreme_scales(problem, oracle, samples100):
-    """Every exit of the v9 LU's fast pivot step (hc_lu9.hpp): pivots below 2^-90
+    """Every exit of the v9 LU's fast pivot step (hc_lu.hpp): pivots below 2^-90
     and at/above 2^120, entries at/above 2^88 (the whole solve runs dense), an
     infinity, NaN at the pivot position, denormals, and structurally sparse
     tracker Jacobians at those scales -- bit-exact against the oracle."""

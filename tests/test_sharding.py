@@ -101,6 +101,20 @@ def test_pass_in_first_chunk_of_rank0(tmp_path):
     assert [r[2:] for r in res] == [[0], [0]]
 
 
+@pytest.mark.timeout(120)
+def test_uneven_chunk_counts_do_not_hang(tmp_path):
+    """17 samples on 2 ranks in chunks of 8: shards 9 / 8 give rank 0 two
+    chunks and rank 1 one.  Every rank must make the same number of flag
+    reductions (rank 1 pads with one that launches nothing); a pass in rank
+    0's last chunk still reaches rank 1."""
+    res = _run(2, 17, 8, [], tmp_path)
+    assert [r[0] for r in res] == [2, 1]
+    assert [r[2:] for r in res] == [[0, 1], [0]]
+    res = _run(2, 17, 8, [8], tmp_path)              # global sample 8 = rank 0's second chunk
+    assert [r[1] for r in res] == [1, 1]
+    assert [r[2:] for r in res] == [[0, 1], [0]]
+
+
 def _pose_worker(rank, world, port, cuts, out_dir):
     """Each rank selects over its shard with the oracle (standing in for the
     device kernel) and the shards are merged through gather_pose_selection."""

@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-# HC_TRIFOCAL_LIB: an alternative build of the same library (A/B experiments)
+# HC_TRIFOCAL_LIB: an alternative build of the same library (A/B experiments,
+# scripts/build_variant.sh)
 LIB_PATH = os.environ.get("HC_TRIFOCAL_LIB") or os.path.join(PKG_DIR, "lib", "libhc_trifocal.so")
 
 NUM_VARS, NUM_PARAMS, NUM_TRACKS = 30, 33, 312
@@ -62,7 +63,8 @@ class hcAbortArgs(C.Structure):
                 ("triplet_edge_locations", C.c_void_p),
                 ("intrinsic_matrix", C.c_void_p),
                 ("found_trifocal_sols", C.c_void_p),
-                ("trifocal_sols_batch_index", C.c_void_p)]
+                ("trifocal_sols_batch_index", C.c_void_p),
+                ("inflight_stop", C.c_int)]
 
 
 _lib = None
@@ -83,12 +85,13 @@ def lib() -> C.CDLL:
         L.hc_trifocal_version.restype = C.c_char_p
         L.hc_last_error_string.restype = C.c_char_p
         for fn in ("hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
-                   "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched"):
+                   "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched"):
             getattr(L, fn).restype = C.c_int
         L.hc_trifocal_2op1p_30x30_track.argtypes = [C.POINTER(hcTrackArgs), C.c_void_p, C.c_size_t, C.c_void_p]
         L.hc_trifocal_2op1p_30x30_track_abort.argtypes = [C.POINTER(hcTrackArgs), C.POINTER(hcAbortArgs),
                                                           C.c_void_p, C.c_size_t, C.c_void_p]
         L.hc_trifocal_read_timings.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        L.hc_trifocal_workspace_status.argtypes = [C.c_void_p]
         L.hc_trifocal_read_timestamps.restype = C.c_int
         L.hc_trifocal_read_timestamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                                   C.POINTER(C.c_double)]
@@ -127,7 +130,7 @@ def check(status: int, what: str) -> None:
 # Exported symbols that include/*.h declare (tests check the library exports all of them).
 DECLARED_SYMBOLS = (
     "hc_trifocal_workspace_size", "hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
-    "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
+    "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
     "hc_last_error_string",
     "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
     "hc_count_triplet_edgels", "hc_read_triplet_edgels", "hc_split_samples", "hc_prepare_target_params",

@@ -114,6 +114,7 @@ GPU_HC_Solver::GPU_HC_Solver(const HC_Settings &S, const std::string &root_dir) 
     Num_Of_Params = S.i("Num_Of_Params", 33);
     Num_Of_Tracks = S.i("Num_Of_Tracks", 312);
     Abort_RANSAC_by_Good_Sol = S.b("Abort_RANSAC_by_Good_Sol", false);
+    Abort_Inflight_Stop = S.b("Abort_Inflight_Stop", false);
     RANSAC_Dataset_Name = S.has("RANSAC_Dataset") ? S.str("RANSAC_Dataset") : "Synthetic";
     Num_Of_GPUs = S.i("Num_Of_GPUs", 1);
     Num_Of_RANSAC_Iterations = S.i("Num_Of_RANSAC_Iterations", 100);
@@ -328,11 +329,13 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
         hcStatus st;
         if (Abort_RANSAC_by_Good_Sol) {
             hcAbortArgs ab;
+            std::memset(&ab, 0, sizeof(ab));
             ab.num_triplet_edgels = Num_Of_Triplet_Edgels;
             ab.triplet_edge_locations = p->d_edgels;
             ab.intrinsic_matrix = p->d_K;
             ab.found_trifocal_sols = p->d_found;
             ab.trifocal_sols_batch_index = p->d_batch_index;
+            ab.inflight_stop = Abort_Inflight_Stop ? 1 : 0;
             st = hc_trifocal_2op1p_30x30_track_abort(&a, &ab, p->d_ws, p->ws_bytes, (hcStream)p->stream);
         } else {
             st = hc_trifocal_2op1p_30x30_track(&a, p->d_ws, p->ws_bytes, (hcStream)p->stream);
@@ -347,6 +350,13 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
         HC_HIP_CHECK(hipStreamSynchronize(p->stream));
     }
     multi_GPUs_time = now_s() - multi_GPUs_time;                                // :446
+    for (PerGPU *p : gpus_) {
+        HC_HIP_CHECK(hipSetDevice(p->dev));
+        const hcStatus st = hc_trifocal_workspace_status(p->d_ws);
+        if (st != HC_SUCCESS)
+            throw std::runtime_error(std::string("GPU-HC tracking failed on device ") + std::to_string(p->dev) +
+                                     ": status " + std::to_string((int)st));
+    }
 
     // Transform_GPUHC_Sols_to_Trifocal_Relative_Pose + get_Solution_with_Maximal_Support
     // (:526-527), on the device before the copies back, outside the tracking timer

@@ -1,9 +1,9 @@
-// hc_eval3.hpp -- v3 polynomial evaluation of the two-paths-per-wave tracker.
+// hc_eval.hpp -- polynomial evaluation of the two-paths-per-wave tracker.
 //
-// Same terms, same operation order as eval_hx2 / eval_ht / eval_h (and the
-// oracle): gpu-idx-evals/dev-eval-indxing-trifocal_2op1p_30x30_LimUnroll_L2Cache.cuh
-// :57-88 (dH/dx), :91-119 (dH/dt), :122-148 (H).  What changes is the
-// instruction count (profiles/r1_v3w4_pmc_summary.json: VALU issue 73 % busy):
+// Same terms, same operation order as the reference and the oracle:
+// gpu-idx-evals/dev-eval-indxing-trifocal_2op1p_30x30_LimUnroll_L2Cache.cuh
+// :57-88 (dH/dx), :91-119 (dH/dt), :122-148 (H).  Lane r of a half-wave
+// evaluates equation row r of its path from compacted per-row term lists:
 //
 //  * term words carry LDS byte offsets relative to the path slot (SlotLDS), so
 //    an operand address is one add (p offsets in 16-bit halves, x offsets in
@@ -20,29 +20,32 @@
 
 #include <stddef.h>
 
-#include "hc_track2.hpp"
+#include "hc_slot.hpp"
 
 namespace hc {
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
-constexpr int HX3_SLOT_CAP = 24;   // per-lane dH/dx terms (this problem: 23); keeps LDS <= 40 KB/WG
+constexpr int HX_SLOT_CAP = 24;   // per-lane dH/dx terms (this problem: 23)
 constexpr int SLOT_OFF_X = (int)offsetof(SlotLDS, x);
 constexpr int SLOT_OFF_P = (int)offsetof(SlotLDS, p);
 constexpr int SLOT_DIF_DELTA = (int)offsetof(SlotLDS, dif) - (int)offsetof(SlotLDS, p);
 static_assert(SLOT_OFF_X + 8 * 31 < 256, "x offsets must fit a byte");
 static_assert(SLOT_OFF_P + 8 * NPP < 65536, "p offsets must fit 16 bits");
 
-// v3 tables, built by the prep kernel next to the v1/v2 tables.
+// Compacted tables, built once per launch by k_prep_tables from the
+// reference's padded unified index (Data_Reader.cpp:167-189).
+//  map[q][r]  (row r): column c -> entry slot (3 bits x 10 columns per word, 6 = structural zero)
 //  hx[k][r] (row r's k-th dH/dx term): .x = off(p[a]) | off(p[b]) << 16
 //                                      .y = off(x[u]) | off(x[v]) << 8 | (int8)coef << 16 | 8*slot << 24 | last << 31
 //  ht[j][r] (row r's j-th dH/dt / H term): .x = off(p[a]) | off(p[b]) << 16
 //                                      .y = off(x[u]) | off(x[v]) << 8 | off(x[w]) << 16 | (int8)coef << 24
-struct TableWS3 {
+struct EvalTables {
     int hx_len;
     int status;
     int pad[2];
-    uint2 hx[HX3_SLOT_CAP * 32];
+    uint32_t map[3][32];
+    uint2 hx[HX_SLOT_CAP * 32];
     uint2 ht[HT_TERMS * 32];
 };
 
@@ -91,20 +94,20 @@ __device__ __forceinline__ HxOps hx_ops(const char *sb, uint2 w) {
     return HxOps{ldp(sb, w.x & 0xFFFFu), ldp(sb, w.x >> 16), ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu)};
 }
 
-// the term loop of eval_hx3: operands are read through sb (x, p of the slot),
+// the term loop of eval_hx: operands are read through sb (x, p of the slot),
 // running sums written through eb (the lane's entry row)
-__device__ __forceinline__ void eval_hx3_terms(const uint2 *s_hx3, const char *sb, char *eb, int r) {
-    uint2 w[HX3_SLOT_CAP];
+__device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb, char *eb, int r) {
+    uint2 w[HX_SLOT_CAP];
 #pragma unroll
-    for (int k = 0; k < EV_WAHEAD; k++) w[k] = s_hx3[k * 32 + r];
+    for (int k = 0; k < EV_WAHEAD; k++) w[k] = s_hx[k * 32 + r];
     HxOps o[EV_AHEAD + 1];
 #pragma unroll
     for (int k = 0; k < EV_AHEAD; k++) o[k] = hx_ops(sb, w[k]);
     pf2 acc = {0.0f, 0.0f};
 #pragma unroll
-    for (int k = 0; k < HX3_SLOT_CAP; k++) {
-        if (k + EV_WAHEAD < HX3_SLOT_CAP) w[k + EV_WAHEAD] = s_hx3[(k + EV_WAHEAD) * 32 + r];
-        if (k + EV_AHEAD < HX3_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
+    for (int k = 0; k < HX_SLOT_CAP; k++) {
+        if (k + EV_WAHEAD < HX_SLOT_CAP) w[k + EV_WAHEAD] = s_hx[(k + EV_WAHEAD) * 32 + r];
+        if (k + EV_AHEAD < HX_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
         const HxOps &q = o[k % (EV_AHEAD + 1)];
         const float co = (float)(int)(int8_t)(uint8_t)(w[k].y >> 16);
         pf2 P = q.pa * pf2{co, co};
@@ -118,19 +121,18 @@ __device__ __forceinline__ void eval_hx3_terms(const uint2 *s_hx3, const char *s
 }
 
 // dH/dx: row r of both paths' Jacobians into rA.  The term loop is fully
-// unrolled over the padded table (HX3_SLOT_CAP words per lane; the caller stages
+// unrolled over the padded table (HX_SLOT_CAP words per lane; the caller stages
 // all of them) and branch-free, so the scheduler can keep several terms' LDS
 // reads in flight: every term stores its running sum -- to its entry slot when
 // it is the entry's last term, else to the lane's structural-zero slot 6 as a
 // scratch word -- and slot 6 is re-zeroed before the gather.
-__device__ __forceinline__ void eval_hx3(cf (&rA)[NV], const uint2 *s_hx3, int hx_len, const uint32_t (&map)[3],
-                                         SlotLDS &S, int r) {
-    (void)hx_len;
+__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t (&map)[3], SlotLDS &S,
+                                        int r) {
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
-    eval_hx3_terms(s_hx3, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
+    eval_hx_terms(s_hx, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
     float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    if (r < NV) ent_row[6] = cmk(z, z);   // structural zero (the v3 LU reuses this block)
+    if (r < NV) ent_row[6] = cmk(z, z);   // structural zero (the LU reuses this block)
     wave_lds_sync();
     // opaque copy: keeps LICM from hoisting the 30 decoded gather addresses out
     // of the path loop (30 VGPRs held across the LU, then spilled)
@@ -151,18 +153,18 @@ __device__ __forceinline__ HtOps ht_ops(const char *sb, uint2 w) {
 }
 
 // dH/dt: b = -sum_j c*(d[a]*p[b] + d[b]*p[a])*x[u]*x[v]*x[w]
-__device__ __forceinline__ cf eval_ht3(const uint2 *s_ht3, const SlotLDS &S, int r) {
+__device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r) {
     const char *sb = reinterpret_cast<const char *>(&S);
     uint2 w[HT_TERMS];
 #pragma unroll
-    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht3[j * 32 + r];
+    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht[j * 32 + r];
     HtOps o[EV_AHEAD + 1];
 #pragma unroll
     for (int j = 0; j < EV_AHEAD; j++) o[j] = ht_ops(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < HT_TERMS; j++) {
-        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht3[(j + EV_WAHEAD) * 32 + r];
+        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht[(j + EV_WAHEAD) * 32 + r];
         if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = ht_ops(sb, w[j + EV_AHEAD]);
         const HtOps &q = o[j % (EV_AHEAD + 1)];
         const float co = (float)((int)w[j].y >> 24);
@@ -181,18 +183,18 @@ __device__ __forceinline__ HOps h_ops(const char *sb, uint2 w) {
 }
 
 // H: b = sum_j c*p[a]*p[b]*x[u]*x[v]*x[w]
-__device__ __forceinline__ cf eval_h3(const uint2 *s_ht3, const SlotLDS &S, int r) {
+__device__ __forceinline__ cf eval_h(const uint2 *s_ht, const SlotLDS &S, int r) {
     const char *sb = reinterpret_cast<const char *>(&S);
     uint2 w[HT_TERMS];
 #pragma unroll
-    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht3[j * 32 + r];
+    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht[j * 32 + r];
     HOps o[EV_AHEAD + 1];
 #pragma unroll
     for (int j = 0; j < EV_AHEAD; j++) o[j] = h_ops(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
 #pragma unroll
     for (int j = 0; j < HT_TERMS; j++) {
-        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht3[(j + EV_WAHEAD) * 32 + r];
+        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht[(j + EV_WAHEAD) * 32 + r];
         if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = h_ops(sb, w[j + EV_AHEAD]);
         const HOps &q = o[j % (EV_AHEAD + 1)];
         const float co = (float)((int)w[j].y >> 24);

@@ -1,0 +1,347 @@
+// hc_lu.hpp -- the tracker's batched 30x30 complex LU solve, two systems per
+// wavefront (one per 32-lane half; lane r owns row r in 60 VGPRs).
+//
+// Semantics: magmaHC/dev-cgesv-batched-small.cuh:38-107 -- partial pivoting
+// on cabs1 = |re| + |im| with first-maximum ties (the pivot search scans the
+// eligible positions in order with a strict '>'), rows relabelled through
+// rowid instead of moved, a zero pivot skips the elimination with recip = 1,
+// back substitution with cuCdivf.  Op for op the spec of DESIGN.md §4, up to
+// the sign of exact zeros (the equivalence class DESIGN.md §4 documents).
+//
+// How one pivot step I runs (common path, both halves at once):
+//  * search: key = bits of |re|+|im| (non-negative floats order like ints),
+//    max over the half with 4 DPP steps + v_permlane16_swap, ballot of the
+//    maxima.  NaN keys take part (positive NaN bits order above every finite
+//    value); a maximum outside the fast reciprocal range (NaN, inf, zero,
+//    tiny, huge) or a tie in either half sends the step to the exact rare
+//    path (NaN at position I wins, first position among ties);
+//  * broadcast: the pivot lane writes its row (the non-zero column chunks),
+//    rhs and rowid into its half's LDS buffer (ds_write_b128), every lane
+//    reads it back (broadcast ds_read_b128);
+//  * 1/pivot: cuCdivf(1, pivot) with v_rcp_f32 + one Newton step, which is
+//    the IEEE quotient for s in [2^-90, 2^120) (exhaustively verified,
+//    scripts/rcp_check.hip, profiles/r1_rcp_check.json); the pivot lane keeps
+//    the factors (o1, o2) for the back substitution;
+//  * one exec region (rows below the pivot): multiplier, right-hand side,
+//    fill-in pattern and the rank-1 update, 2 v_pk_fma_f32 per element.
+//
+// Structural sparsity.  The trifocal Jacobian is sparse (170 of 900 entries
+// carry terms) and partial-pivot elimination fills it in only partly: on
+// tracker Jacobians 64 % of the pivot-row entries a step broadcasts are exact
+// zeros.  Each lane keeps the structural pattern of its row (bit c: column c
+// may be non-zero) -- initially the columns with index terms, then OR-ed with
+// the pivot rows' patterns whenever the row takes a multiple of one
+// (fill-in).  A chunk of columns that is zero in both pivot rows of the wave
+// is neither written, read nor used in the update (one uniform branch).
+// Exactness: a structurally zero entry holds an exact zero while no product
+// is infinite or NaN, and a - l*0 == a up to the sign of a zero.  Guarantees:
+//  * the solve runs sparse only if every entry is finite with |re|, |im| <
+//    2^88 (wave-uniform check; else every step is dense).  Pivoting on
+//    |re|+|im| bounds every multiplier by sqrt(2) and the element growth by
+//    (1+sqrt(2))^29 < 2^37, so no intermediate can overflow;
+//  * a step whose 1/pivot leaves the fast range (|pivot| < 2^-90: 1/pivot may
+//    overflow; zero or NaN pivot) is executed densely and makes the pattern
+//    of every row below it dense.
+//
+// The buffer aliases the per-path dH/dx entry block (SlotLDS::ent), which is
+// dead between the gather of the Jacobian into registers and the next eval.
+#pragma once
+
+#include "hc_eval.hpp"
+
+namespace hc {
+
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+struct alignas(16) LUBuf {
+    cf row[32];    // current pivot row: [0..29] A, [30] rhs, [31].x = rowid (int bits); x in the back sub
+};
+static_assert(sizeof(LUBuf) <= sizeof(cf) * NV * 7, "LUBuf must fit in SlotLDS::ent");
+static_assert(offsetof(SlotLDS, ent) % 16 == 0, "SlotLDS::ent must be 16-B aligned");
+
+#ifndef HC_LU_CHUNK
+#define HC_LU_CHUNK 4
+#endif
+constexpr int LU_CHUNK = HC_LU_CHUNK;   // columns per skippable group (even)
+
+// Correctly rounded 1/s for s in [2^-90, 2^120): v_rcp_f32 plus one Newton
+// step (bit-identical to hipcc's div_scale / div_fmas / div_fixup sequence
+// for every float in that range).
+__device__ __forceinline__ float rcp_rn(float s) {
+    const float r0 = __builtin_amdgcn_rcpf(s);
+    const float e0 = __builtin_fmaf(-s, r0, 1.0f);
+    return __builtin_fmaf(e0, r0, r0);
+}
+// s in the fast reciprocal range, on the bit pattern of a non-negative float
+// (NaN and the -1 "no candidate" key fall outside)
+__device__ __forceinline__ bool rcp_fast_bits(int bits) {
+    return (uint32_t)(bits - 0x12800000) < (uint32_t)(0x7B800000 - 0x12800000);
+}
+
+__device__ __forceinline__ void st4(cf *p, cf a, cf b) {
+    f4v v = {a.x, a.y, b.x, b.y};
+    *reinterpret_cast<f4v *>(p) = v;
+}
+__device__ __forceinline__ void ld4(const cf *p, cf &a, cf &b) {
+    const f4v v = *reinterpret_cast<const f4v *>(p);
+    a = cmk(v.x, v.y);
+    b = cmk(v.z, v.w);
+}
+
+// max over each 32-lane half: DPP inside 16-lane rows, then v_permlane16_swap
+// across the row pair (VALU; no LDS round trip unlike ds_swizzle)
+__device__ __forceinline__ int half_max_int_p16(int v) {
+    v = max(v, dpp_i<DPP_QP_1032>(v));
+    v = max(v, dpp_i<DPP_QP_2301>(v));
+    v = max(v, dpp_i<DPP_ROW_HALF_MIRROR>(v));
+    v = max(v, dpp_i<DPP_ROW_MIRROR>(v));
+    const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return max((int)sw[0], (int)sw[1]);
+}
+
+// structural pattern of row r from its column->entry-slot map (slot 6 = zero)
+__device__ __forceinline__ uint32_t row_pattern(const uint32_t (&map)[3]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int c = 0; c < NV; c++)
+        if (((map[c / 10] >> (3 * (c % 10))) & 7u) != 6u) m |= 1u << c;
+    return m;
+}
+
+// reciprocals (o1, o2) of the cuCdivf factors of the pivot a lane owns, kept
+// from the forward step that chose it (brs, bis = pivot * o1 are recomputed
+// from the pivot element, which stays in the owner's rA)
+struct PivF { pf2 oo; };
+
+// cuCdivf(1, y) for s = |y.re| + |y.im| in the fast range, in packed FP32 with
+// the spec's ops: o1 = 1/s, (brs, bis) = y*o1, o2 = 1/(brs*brs + bis*bis),
+// 1/y = ((o1*brs)*o2, (-(o1*bis))*o2); -(o1*bis) is computed as o1*(-bis)
+// (IEEE: the same value).  oo returns (o1, o2).
+__device__ __forceinline__ pf2 recip_fast(pf2 y, float s, pf2 &oo) {
+    oo.x = rcp_rn(s);
+    pf2 bb, sq, q, r;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(bb) : "v"(y), "v"(oo));
+    asm("v_pk_mul_f32 %0, %1, %1" : "=v"(sq) : "v"(bb));
+    oo.y = rcp_rn(sq.x + sq.y);
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(q) : "v"(oo), "v"(bb));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(q), "v"(oo));
+    return r;
+}
+
+// cdiv_apply(b, f) = cuCdivf(b, pivot) in packed FP32, op for op:
+// (brs, bis) = pivot*o1; (ars, ais) = b*o1; re = (ars*brs + ais*bis)*o2; im = (ais*brs - ars*bis)*o2
+__device__ __forceinline__ pf2 pcdiv_apply(pf2 b, pf2 piv, const PivF &f) {
+    pf2 bb, a, t1, t2, s, q;
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(bb) : "v"(piv), "v"(f.oo));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(a) : "v"(b), "v"(f.oo));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(t1) : "v"(a), "v"(bb));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[1,1] op_sel_hi:[0,1]" : "=v"(t2) : "v"(a), "v"(bb));
+    asm("v_pk_add_f32 %0, %1, %2 neg_hi:[0,1]" : "=v"(s) : "v"(t1), "v"(t2));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(q) : "v"(s), "v"(f.oo));
+    return q;
+}
+
+// Column groups of step I: a leading single column when I+1 is odd, then
+// groups of CH (even) columns.  The pivot lanes write, and the update reads,
+// exactly these groups.
+template <int CH>
+struct LuChunks {
+    static constexpr int single(int I) { return ((I + 1) & 1) && (I + 1 < NV) ? 1 : 0; }
+    static constexpr int start(int I, int k) { return k < single(I) ? I + 1 : I + 1 + single(I) + (k - single(I)) * CH; }
+    static constexpr int len(int I, int k) {
+        return k < single(I) ? 1 : ((NV - start(I, k)) < CH ? (NV - start(I, k)) : CH);
+    }
+    static constexpr int count(int I) { return single(I) + (NV - (I + 1 + single(I)) + CH - 1) / CH; }
+    static constexpr uint32_t mask(int I, int k) { return ((1u << len(I, k)) - 1u) << start(I, k); }
+};
+
+// pivot lane: row elements of the groups of step I that are non-zero in some
+// pivot row of the wave
+template <int I, int K>
+__device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, LUBuf &L) {
+    using C = LuChunks<LU_CHUNK>;
+    if constexpr (K < C::count(I)) {
+        constexpr int J = C::start(I, K), N = C::len(I, K);
+        if (pmw & C::mask(I, K)) {
+            if constexpr (N == 1) {
+                L.row[J] = rA[J];
+            } else {
+#pragma unroll
+                for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
+            }
+        }
+        lu_put_row<I, K + 1>(rA, pmw, L);
+    }
+}
+
+// a_j -= l * u_j for the groups K.. of step I (the caller is inside the
+// below-the-pivot exec region)
+template <int I, int K>
+__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, const LUBuf &L) {
+    using C = LuChunks<LU_CHUNK>;
+    if constexpr (K < C::count(I)) {
+        constexpr int J = C::start(I, K), N = C::len(I, K);
+        if (pmw & C::mask(I, K)) {
+            cf u[N];
+            if constexpr (N == 1) {
+                u[0] = L.row[J];
+            } else {
+#pragma unroll
+                for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
+            }
+#pragma unroll
+            for (int q = 0; q < N; q++) {
+                const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
+                rA[J + q] = cmk(v.x, v.y);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        lu_update<I, K + 1>(rA, l, pmw, L);
+    }
+}
+
+template <int I>
+__device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool all_dense, int lane,
+                                           int r, int hb, bool row_lane, PivF &my, LUBuf &L) {
+    if constexpr (I < NV) {
+        const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
+        const bool elig = rowid >= I && row_lane;
+        bool is_piv;
+        float piv_abs;
+        int pl0, pl1;   // pivot lanes of the two halves
+        bool dense;
+        const int key = elig ? __float_as_int(v) : -1;
+        const int mx = half_max_int_p16(key);
+        const unsigned long long m = __builtin_amdgcn_ballot_w64(key == mx);
+        const unsigned long long bad = __builtin_amdgcn_ballot_w64(!rcp_fast_bits(mx));
+        const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
+        if (__builtin_expect(((mlo & (mlo - 1u)) | (mhi & (mhi - 1u))) != 0u || bad != 0ull || all_dense, 0)) {
+            // rare: NaN at position I wins (:57-64); exact ties: first position wins
+            const bool isn = v != v;
+            const int key2 = (elig && !isn) ? __float_as_int(v) : -1;
+            const int mx2 = half_max_int_p16(key2);
+            const unsigned long long m2 = __builtin_amdgcn_ballot_w64(key2 == mx2);
+            const unsigned long long nanm = __builtin_amdgcn_ballot_w64(isn) & __builtin_amdgcn_ballot_w64(rowid == I);
+            const unsigned nlo = (unsigned)nanm, nhi = (unsigned)(nanm >> 32);
+            const unsigned mine_m = hb ? (unsigned)(m2 >> 32) : (unsigned)m2, mine_n = hb ? nhi : nlo;
+            const int c2 = ((mine_m >> r) & 1u) ? rowid : (1 << 20);
+            const int mn = half_min_i(c2);
+            const unsigned long long w = __builtin_amdgcn_ballot_w64(row_lane && rowid == mn);
+            const unsigned wm = hb ? (unsigned)(w >> 32) : (unsigned)w;
+            const int pl = mine_n ? hb + __builtin_ctz(mine_n) : hb + (wm ? __builtin_ctz(wm) : 0);
+            is_piv = lane == pl;
+            piv_abs = mine_n ? __builtin_nanf("") : __int_as_float(mx2);
+            const unsigned long long pm = __builtin_amdgcn_ballot_w64(is_piv);
+            pl0 = __builtin_ctz((unsigned)pm | 0x80000000u);
+            pl1 = 32 + __builtin_ctz((unsigned)(pm >> 32) | 0x80000000u);
+            dense = all_dense || __builtin_amdgcn_ballot_w64(!rcp_fast_bits(__float_as_int(piv_abs))) != 0ull;
+        } else {
+            is_piv = key == mx;
+            piv_abs = __int_as_float(mx);
+            pl0 = __builtin_ctz(mlo | 0x80000000u);
+            pl1 = 32 + __builtin_ctz(mhi | 0x80000000u);
+            dense = false;
+        }
+        // structural patterns of the two pivot rows (wave-uniform)
+        const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl0);
+        const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
+        constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
+        const uint32_t pmw = dense ? FULL : ((pp0 | pp1) & FULL);
+        if (is_piv) {                                          // pivot row -> buffer
+            L.row[I] = rA[I];
+            lu_put_row<I, 0>(rA, pmw, L);
+            L.row[30] = rB;
+            L.row[31].x = __int_as_float(rowid);
+        }
+        wave_lds_sync();
+        const cf sxi = L.row[I];
+        cf sB0, pr;
+        ld4(&L.row[30], sB0, pr);
+        const int piv_pos = __float_as_int(pr.x);
+        if (is_piv) rowid = I;                                 // :70-82
+        else if (rowid == I) rowid = piv_pos;
+        // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
+        cf reg;
+        divf f;
+        if (__builtin_expect(!dense, 1)) {
+            pf2 oo;
+            const pf2 rg = recip_fast(pf2{sxi.x, sxi.y}, piv_abs, oo);
+            reg = cmk(rg.x, rg.y);
+            f.o1 = oo.x;
+            f.o2 = oo.y;
+        } else {
+            f = cdiv_factors(sxi);
+            reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
+        }
+        if (is_piv) my.oo = pf2{f.o1, f.o2};
+        // opaque: the select chain must be resolved here, not carried as 30
+        // per-step factor pairs into the back substitution
+        asm volatile("" : "+v"(my.oo));
+        const bool below = rowid > I;                          // :86-93
+        // one exec-masked region per step: multiplier, right-hand side,
+        // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
+        // below whose column I may be non-zero takes the pivot patterns (both
+        // halves': a superset of its own pivot row's); after a dense step
+        // nothing is known zero.
+        const uint32_t pmwd = dense ? 0xFFFFFFFFu : pmw;
+        if (below) {
+            const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+            const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
+            rB = cmk(bp.x, bp.y);
+            pat |= (((pat >> I) & 1u) != 0u || dense) ? pmwd : 0u;
+            lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, L);
+        }
+        lu_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+    }
+}
+
+// back substitution (:97-106): the lane whose final rowid is I owns position I
+// and divides with the factors it kept from the forward step; x_I reaches the
+// lanes of its half with v_readlane (owner lane of each half found by a
+// ballot of the final row ids)
+template <int I>
+__device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, int hb) {
+    if constexpr (I >= 0) {
+        const unsigned long long own = __builtin_amdgcn_ballot_w64(rowid == I);
+        const int o0 = __builtin_ctz((unsigned)own | 0x80000000u);
+        const int o1 = 32 + __builtin_ctz((unsigned)(own >> 32) | 0x80000000u);
+        const pf2 q = pcdiv_apply(pf2{rB.x, rB.y}, pf2{rA[I].x, rA[I].y}, my);
+        const float x0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.x), o0));
+        const float y0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o0));
+        const float x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.x), o1));
+        const float y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o1));
+        const cf xi = hb ? cmk(x1, y1) : cmk(x0, y0);
+        if (rowid < I) {
+            const pf2 w = pcmsub(pf2{rB.x, rB.y}, pf2{xi.x, xi.y}, pf2{rA[I].x, rA[I].y});
+            rB = cmk(w.x, w.y);
+        }
+        if (rowid == I) rB = xi;   // the owner keeps its x_I (returned below)
+        lu_backward<I - 1>(rA, rB, rowid, my, hb);
+    }
+}
+
+// Solves the system of each half: lane r holds row r of A in rA and b_r in
+// rB; pattern = the structural pattern of row r.  Returns x_r in lane r.  L is
+// this half's buffer (16-B aligned).
+__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L) {
+    // every entry finite and below 2^88 in magnitude (NaN fails the compare)
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < NV; c++)
+        ok = ok && __builtin_fabsf(rA[c].x) < 0x1p88f && __builtin_fabsf(rA[c].y) < 0x1p88f;
+    const bool all_dense = __builtin_amdgcn_ballot_w64(!ok) != 0ull;   // then every step is dense
+    const int r = lane & 31, hb = lane & 32;
+    const bool row_lane = r < NV;
+    int rowid = row_lane ? r : 99;   // padding lanes never pivot
+    uint32_t pat = row_lane ? pattern : 0u;
+    PivF my{pf2{0.0f, 0.0f}};
+    lu_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+    lu_backward<NV - 1>(rA, rB, rowid, my, hb);
+    // lane r returns x_r: the owner of position r holds it in rB
+    wave_lds_sync();
+    if (row_lane) L.row[rowid] = rB;
+    wave_lds_sync();
+    return L.row[row_lane ? r : 0];
+}
+
+}  // namespace hc

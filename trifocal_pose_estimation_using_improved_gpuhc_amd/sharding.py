@@ -46,24 +46,41 @@ def chunks(count: int, chunk_samples: int) -> List[Tuple[int, int]]:
 
 
 def run_abort_chunks(launch_chunk: Callable[[int, int, int], None], flag, count: int, chunk_samples: int,
-                     group=None) -> int:
+                     group=None, stream=None) -> int:
     """Early-stop protocol over this rank's samples.
 
     launch_chunk(k, offset, n) enqueues chunk k (samples [offset, offset+n) of
     the shard); the launch reads `flag` when it starts and sets it when a
     passing hypothesis is found.  After each launch the flag is max-reduced
-    over all ranks (stream-ordered for RCCL; synchronous for gloo).  Returns
-    the number of chunks enqueued (always all of them: a chunk that starts
-    with the flag set skips its paths on the device, so no host round trip is
-    needed to stop).
+    over all ranks.  Every rank makes the same number of reductions -- the
+    largest chunk count over the ranks (one extra all_reduce agrees on it), so
+    a rank whose shard is a chunk shorter (uneven sample counts) pads with
+    reductions that launch nothing instead of leaving its peers waiting.  With
+    RCCL the reductions and the launches are ordered on `stream` (the launch
+    stream; default: the current stream), so nothing synchronises with the
+    host between chunks; with gloo they are synchronous.  Returns the number
+    of chunks this rank launched (all of its own: a chunk that starts with the
+    flag set skips its paths on the device).
     """
+    import contextlib
+
+    import torch
     import torch.distributed as dist
     parts = chunks(count, chunk_samples)
     multi = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
-    for k, (off, n) in enumerate(parts):
-        launch_chunk(k, off, n)
+    on_gpu = getattr(flag, "is_cuda", False)
+    ctx = torch.cuda.stream(stream) if (on_gpu and stream is not None) else contextlib.nullcontext()
+    with ctx:
+        rounds = len(parts)
         if multi:
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+            n = torch.tensor([rounds], dtype=torch.int64, device=flag.device)
+            dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
+            rounds = int(n.item())
+        for k in range(rounds):
+            if k < len(parts):
+                launch_chunk(k, *parts[k])
+            if multi:
+                dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     return len(parts)
 
 

@@ -101,12 +101,15 @@ class DeviceTracker:
 
     def launch(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, abort: bool = False,
                stream: torch.cuda.Stream | None = None, workspace: torch.Tensor | None = None,
-               sample_offset: int = 0, num_samples: int | None = None) -> None:
+               sample_offset: int = 0, num_samples: int | None = None, inflight_stop: bool = False) -> None:
         """Enqueue one tracking run on `stream` (no synchronisation).
 
         Samples [sample_offset, sample_offset + num_samples) of `target`/`diff`
         are tracked into the matching rows of `r` (defaults: all of them); the
-        launch's batch ids (abort-mode batch_index values) are local to it."""
+        launch's batch ids (abort-mode batch_index values) are local to it.
+        inflight_stop (abort mode): paths in flight also stop once a pose is
+        found (hcAbortArgs::inflight_stop; default: the reference's semantics,
+        they run to completion)."""
         if num_samples is None:
             num_samples = target.shape[0] - sample_offset
         if num_samples < 0 or sample_offset < 0 or sample_offset + num_samples > target.shape[0] or \
@@ -142,6 +145,7 @@ class DeviceTracker:
             ab.intrinsic_matrix = self.K.data_ptr()
             ab.found_trifocal_sols = r.found.data_ptr()
             ab.trifocal_sols_batch_index = r.batch_index[p0:p1].data_ptr()
+            ab.inflight_stop = 1 if inflight_stop else 0
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track_abort")
         else:
@@ -152,20 +156,28 @@ class DeviceTracker:
         return torch.zeros(self.ws_bytes, dtype=torch.uint8, device=self.device)
 
     def launch_abort_chunked(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, chunk_samples: int,
-                             workspaces: list, group=None, stream: torch.cuda.Stream | None = None) -> list:
+                             workspaces: list, group=None, stream: torch.cuda.Stream | None = None,
+                             inflight_stop: bool = False) -> list:
         """Abort-mode run of all of target's samples in chunks, with the
-        cross-rank early-stop flag (sharding.run_abort_chunks).  workspaces:
-        one per chunk (grown as needed).  Returns the (offset, count) chunks."""
+        cross-rank early-stop flag (sharding.run_abort_chunks): the launches
+        and the flag reductions share one stream.  workspaces: one per chunk
+        (grown as needed).  Returns the (offset, count) chunks."""
         from . import sharding
         parts = sharding.chunks(target.shape[0], chunk_samples)
         while len(workspaces) < len(parts):
             workspaces.append(self.new_workspace())
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
 
         def one(k, off, n):
-            self.launch(target, diff, r, abort=True, stream=stream, workspace=workspaces[k], sample_offset=off,
-                        num_samples=n)
-        sharding.run_abort_chunks(one, r.found, target.shape[0], chunk_samples, group=group)
+            self.launch(target, diff, r, abort=True, stream=s, workspace=workspaces[k], sample_offset=off,
+                        num_samples=n, inflight_stop=inflight_stop)
+        sharding.run_abort_chunks(one, r.found, target.shape[0], chunk_samples, group=group, stream=s)
         return parts
+
+    def workspace_status(self, workspace: torch.Tensor | None = None) -> None:
+        """Raises HCError if the last launch on workspace rejected the index table."""
+        ws = workspace if workspace is not None else self.workspace
+        _abi.check(self.L.hc_trifocal_workspace_status(C.c_void_p(ws.data_ptr())), "hc_trifocal_workspace_status")
 
     def read_timestamps(self, workspace: torch.Tensor | None = None):
         """(start_ticks, found_ticks, tick_hz) of the last launch on workspace."""
@@ -175,14 +187,16 @@ class DeviceTracker:
                    "hc_trifocal_read_timestamps")
         return a.value, b.value, hz.value
 
-    def track(self, target: np.ndarray, diff: np.ndarray, abort: bool = False, stats: bool = True) -> TrackResult:
-        """Synchronous convenience wrapper: H2D params, reset tracks, launch, sync."""
+    def track(self, target: np.ndarray, diff: np.ndarray, abort: bool = False, stats: bool = True,
+              inflight_stop: bool = False) -> TrackResult:
+        """Synchronous convenience wrapper: H2D params, reset tracks, launch, sync, status check."""
         tgt = torch.from_numpy(np.ascontiguousarray(target, np.float32)).to(self.device)
         dif = torch.from_numpy(np.ascontiguousarray(diff, np.float32)).to(self.device)
         r = self.allocate(tgt.shape[0], stats=stats, abort=abort)
         self.reset_tracks(r)
-        self.launch(tgt, dif, r, abort=abort)
+        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop)
         torch.cuda.synchronize(self.device)
+        self.workspace_status()
         return r
 
     def first_found_seconds(self) -> float:
