@@ -13,8 +13,12 @@ outputs pin the oracle so later rounds (and the GPU box, which has no
   pose_N100_seed0.npz   pose recovery / maximal support over the GPU-HC tracks of
                         the 100 samples: the candidate paths' tracks, their inlier counts, the
                         selected path / inliers / pose per view and its GT residuals
+  gpuhc_noisy1px_N100.npz  config 5 inputs: Triplet_Edgels_000 with sigma = 1 px noise
+                        (noise seed 20250215, the bench's first trial), samples srand(0), 100
+                        samples: per-path flags / counts / hashes, the scoring of every
+                        converged path, and the maximal-support selection with its GT residuals
 
-Run:  python tests/golden/make_golden.py [--only pose]   (takes ~1-2 min on 8 cores)
+Run:  python tests/golden/make_golden.py [--only pose|noisy]   (takes ~1-2 min on 8 cores)
 """
 import os
 import sys
@@ -61,6 +65,33 @@ def pose_fixture(tr, conv, loc, K):
     print("pose: candidates", sel["num_candidates"], "paths", sel["path21"], sel["path31"], "residuals", res, ok)
 
 
+NOISE_SEED = 20250215   # synthcurves.DEFAULT_SEED
+
+
+def noisy_fixture(ss, sp, U, loc, tan, K):
+    gt21 = O.read_floats(os.path.join(RANS, "GT_Poses21", "GT_Poses21_000.txt"), 12)
+    gt31 = O.read_floats(os.path.join(RANS, "GT_Poses31", "GT_Poses31_000.txt"), 12)
+    nloc = O.add_pixel_noise(loc, K, 1.0, NOISE_SEED)
+    tgt, dif, picked = O.prepare_target_params(0, [100], nloc, tan, sp)
+    tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
+    conv_ids = np.nonzero(conv)[0]
+    scores = np.array([O.score_hypothesis(tr[b], nloc, K) for b in conv_ids], dtype=np.int64).reshape(-1, 3)
+    inl, sel = O.pose_support(tr, conv, nloc, K)
+    res, ok = O.pose_residuals(gt21, gt31, sel)
+    np.savez_compressed(os.path.join(HERE, "gpuhc_noisy1px_N100.npz"),
+                        target=tgt, diff=dif, picked=picked,
+                        conv=conv, inf=inf, steps=st["steps"].astype(np.int16),
+                        corrections=st["corrections"].astype(np.int16), hash=track_hash(tr),
+                        tracks_s01=tr[:624], counts=np.array(O.count_solutions(tr, conv, inf)),
+                        scored_ids=conv_ids.astype(np.int32), scored=scores.astype(np.int32),
+                        cand_inliers=inl[inl[:, 0] >= 0], num_candidates=np.int32(sel["num_candidates"]),
+                        path=np.array([sel["path21"], sel["path31"]], np.int32),
+                        inliers=np.array([sel["inliers21"], sel["inliers31"]], np.int32),
+                        residuals=res, success=np.bool_(ok))
+    print("noisy 1px: counts", O.count_solutions(tr, conv, inf), "passing", int(scores[:, 0].sum()) if len(scores) else 0,
+          "candidates", sel["num_candidates"], "paths", sel["path21"], sel["path31"], "residuals", res, ok)
+
+
 def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ss, sp, dhdx, dhdt = O.read_problem(PROB)
@@ -72,6 +103,10 @@ def main():
         tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
         pose_fixture(tr, conv, loc, K)
         return
+    if only in (None, "noisy"):
+        noisy_fixture(ss, sp, U, loc, tan, K)
+        if only == "noisy":
+            return
     np.savez_compressed(os.path.join(HERE, "samples_seed0.npz"), picked=picked, target=tgt, diff=dif)
 
     tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)

@@ -214,3 +214,20 @@ def test_scoring_finds_ground_truth_pose(problem, ransac0, oracle):
     Rgt = ransac0.pose21[:9].reshape(3, 3).astype(np.float64)
     ang = np.arccos(np.clip((np.trace(R.T @ Rgt) - 1) / 2, -1, 1))
     assert ang < 0.1, ang
+
+
+def test_residual_gate_on_golden_candidates(problem):
+    """Gate 2 on the CPU: the converged real candidate solutions of
+    the golden config-2 run (oracle tracks == HIP tracks bit for bit) satisfy the
+    target system in FP64 to a relative residual <= 1e-4; the GT solution to ~1e-7."""
+    import os
+
+    from residual import RESIDUAL_TOL, relative_residuals
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import load_ransac_data, prepare_target_params
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "pose_N100_seed0.npz"))
+    tgt, _, _ = prepare_target_params(problem, load_ransac_data(0), seed=0, num_samples=100)
+    worst = [float(relative_residuals(problem.dHdt_index, x, tgt[b // 312]).max())
+             for b, x in zip(g["cand_ids"], g["cand_tracks"])]
+    assert len(worst) == int(g["num_candidates"]) and max(worst) <= RESIDUAL_TOL
+    best = int(np.nonzero(g["cand_ids"] == g["path"][0])[0][0])
+    assert worst[best] < 1e-5
