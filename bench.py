@@ -37,8 +37,17 @@ sys.path.insert(0, ROOT)
 # complex add 2, real x complex 2, complex div 11)
 FLOP_PRED_STAGE = 104.3e3    # Hx 12,276 + Ht 12,960 + LU 78,670 + axpys ~360
 FLOP_CORR_STAGE = 101.3e3    # Hx 12,276 + H 10,080 + LU 78,670 + update/norms ~300
-FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak == FP32 MFMA peak
+# The LU's rank-1 updates are 8555 element updates (8 FLOP each = 68,440 FLOP)
+# of the 78,670 in the dense algorithm the reference runs.  The structurally
+# sparse LU executes only the column groups that are non-zero in a pivot row
+# of the wave: 5,012.6 elements per solve on config 2 (0.586 of dense), measured
+# by the HC_DIAG_LUWORK build (scripts/lu_work.py, profiles/r2d_lu_work.json).
+LU_UPDATE_DENSE_FLOP = 68440.0
+LU_UPDATE_EXECUTED_FRACTION = 0.5859
+LU_EXEC_SAVING = LU_UPDATE_DENSE_FLOP * (1.0 - LU_UPDATE_EXECUTED_FRACTION)
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak (64 FLOP/clk/SIMD) == FP32 MFMA peak
 HBM_PEAK_GBS = 8000.0
+TRACK_KERNEL = "void hc::k_track<false, 5, true>(hc::KArgs)"
 
 
 def parse():
@@ -57,10 +66,15 @@ def parse():
     ap.add_argument("--noisy-trials", type=int, default=10,
                     help="config 5: RANSAC runs on sigma=1px noisy synthcurves (pose success rate); 0 disables")
     ap.add_argument("--noisy-sigma", type=float, default=1.0)
-    ap.add_argument("--streams", type=int, default=4,
+    ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the timed steps rotate over: step i runs on stream i %% streams with its own "
-                         "track buffers and workspace, so one batch's tail overlaps the next batch's start "
-                         "(1 = strictly serial launches)")
+                         "track buffers and workspace (1 = strictly serial launches, the reference's timer scope: "
+                         "one launch -> sync per RANSAC run, GPU_HC_Solver.cpp:384,446)")
+    ap.add_argument("--pipelined-streams", type=int, default=4,
+                    help="also time the same steps overlapped on this many streams (one batch's tail overlaps the "
+                         "next batch's start); reported as config.pipelined_paths_per_s, 0 disables")
+    ap.add_argument("--cpu-samples-4t", type=int, default=40,
+                    help="samples of the 4-thread CPU-HC run (the reference's Num_Of_Cores default)")
     return ap.parse_args()
 
 
@@ -96,37 +110,47 @@ def main():
     res = tr.allocate(S, stats=True)
     stream = torch.cuda.current_stream(dev)
 
-    # step i: batch i on stream i % NS with its own buffers and workspace (independent
+    # step i: batch i on stream i % ns with its own buffers and workspace (independent
     # RANSAC batches; a stream reuses its buffers only after its previous launch)
     NS = max(1, args.streams)
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(NS - 1)]
-    bufs = [res] + [tr.allocate(S, stats=True) for _ in range(NS - 1)]
-    wss = [tr.workspace] + [tr.new_workspace() for _ in range(NS - 1)]
+    NP = max(NS, args.pipelined_streams)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
+    bufs = [res] + [tr.allocate(S, stats=True) for _ in range(NP - 1)]
+    wss = [tr.workspace] + [tr.new_workspace() for _ in range(NP - 1)]
 
-    def step(i):
-        k = i % NS
+    def step(i, ns):
+        k = i % ns
         with torch.cuda.stream(streams[k]):
             tr.reset_tracks(bufs[k])
         tr.launch(tgt, dif, bufs[k], stream=streams[k], workspace=wss[k])
 
-    for i in range(args.warmup):
-        step(i)
-    torch.cuda.synchronize(dev)
+    def timed(ns):
+        """W untimed warmup steps, then K steps bracketed by barrier + sync; max over ranks."""
+        for i in range(args.warmup):
+            step(i, ns)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(i, ns)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        for k in range(1, min(ns, args.steps)):   # every batch is the same work: identical results on every stream
+            if not (torch.equal(bufs[k].converge, res.converge) and torch.equal(bufs[k].stats, res.stats)
+                    and torch.equal(bufs[k].tracks, res.tracks)):
+                raise RuntimeError("streams disagree")
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el
 
-    # timed region: barrier + sync on both sides
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(i)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    for k in range(1, NS):   # every batch is the same work: identical results on every stream
-        if not (torch.equal(bufs[k].converge, res.converge) and torch.equal(bufs[k].stats, res.stats)):
-            raise RuntimeError("streams disagree")
+    elapsed = timed(NS)
+    pipe_elapsed = timed(args.pipelined_streams) if args.pipelined_streams > 1 else None
 
     # kernel time of one launch alone (serial, HIP events on the launch stream): the
     # roofline's denominator and the latency of one batch
@@ -158,21 +182,16 @@ def main():
     host = res.host()
     steps_sum = int(host["stats"]["steps"].astype(np.int64).sum())
     corr_sum = int(host["stats"]["corrections"].astype(np.int64).sum())
-    flops = steps_sum * 4 * FLOP_PRED_STAGE + corr_sum * FLOP_CORR_STAGE
+    flops = steps_sum * 4 * FLOP_PRED_STAGE + corr_sum * FLOP_CORR_STAGE          # dense-LU convention
+    flops_exec = flops - (steps_sum * 4 + corr_sum) * LU_EXEC_SAVING               # LU updates as executed
     from trifocal_pose_estimation_using_improved_gpuhc_amd import count_solutions
     counts = count_solutions(host["tracks"], host["converge"], host["infinity"])
 
-    t_max = elapsed
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        t_max = float(tt.item())
-        fl = torch.tensor([flops, float(np.median(launch_ms))], dtype=torch.float64, device=dev)
-        dist.all_reduce(fl, op=dist.ReduceOp.SUM)
-
+    t_max = elapsed                 # already the max over ranks
     ms_per_step = t_max / args.steps * 1e3
     paths = 312 * S * world
     value = paths / (ms_per_step / 1e3)
+    pipelined = None if pipe_elapsed is None else paths * args.steps / pipe_elapsed
 
     # ---- early abort (config 3 at N=1, config 4 at N=8): time-to-first-good-pose.
     # Every rank tracks its gpu-major shard of abort_samples*world samples in
@@ -189,38 +208,45 @@ def main():
         tr.set_ransac_data(data)
         ra = tr.allocate(cnt, stats=True, abort=True)
         wss = []
-        ttfp, wall, tracked = [], [], []
-        for _ in range(3):
-            tr.reset_tracks(ra)
-            torch.cuda.synchronize(dev)
-            if world > 1:
-                dist.barrier()
-            w0 = time.perf_counter()
-            tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream)
-            torch.cuda.synchronize(dev)
-            w = time.perf_counter() - w0
-            hz = tr.read_timestamps(wss[0])[2]
-            f = sharding.first_found_seconds([tr.read_timestamps(x)[:2] for x in wss[:len(sharding.chunks(cnt, args.abort_chunk))]], hz)
-            n_tr = int((ra.stats[:, 0] > 0).sum().item())
-            if world > 1:
-                v = torch.tensor([f if f >= 0 else 1e30, -w, -float(n_tr)], dtype=torch.float64, device=dev)
-                dist.all_reduce(v, op=dist.ReduceOp.MIN)
-                f, w = float(v[0].item()), -float(v[1].item())
-                f = -1.0 if f >= 1e29 else f
-                nt = torch.tensor([n_tr], dtype=torch.int64, device=dev)
-                dist.all_reduce(nt)
-                n_tr = int(nt.item())
-            ttfp.append(f)
-            wall.append(w)
-            tracked.append(n_tr)
-        found = bool(ra.found.item())
-        abort_info = {"samples_total": Sa * world, "samples_per_gpu": Sa, "chunk_samples": args.abort_chunk,
-                      "found": found,
-                      "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3) if found else None,
-                      "kernel_exit_wall_ms": round(float(np.median(wall)) * 1e3, 3),
-                      "paths_tracked": int(np.median(tracked)),
-                      "note": "device clock (s_memrealtime) from the first chunk's start, min over ranks; "
-                              "wall = host time to the all-GPU sync, max over ranks"}
+        abort_info = {"samples_total": Sa * world, "samples_per_gpu": Sa, "chunk_samples": args.abort_chunk}
+        for inflight in (False, True):
+            ttfp, wall, tracked = [], [], []
+            for _ in range(3):
+                tr.reset_tracks(ra)
+                torch.cuda.synchronize(dev)
+                if world > 1:
+                    dist.barrier()
+                w0 = time.perf_counter()
+                tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream, inflight_stop=inflight)
+                torch.cuda.synchronize(dev)
+                w = time.perf_counter() - w0
+                hz = tr.read_timestamps(wss[0])[2]
+                f = sharding.first_found_seconds([tr.read_timestamps(x)[:2]
+                                                  for x in wss[:len(sharding.chunks(cnt, args.abort_chunk))]], hz)
+                n_tr = int((ra.stats[:, 0] > 0).sum().item())
+                if world > 1:
+                    v = torch.tensor([f if f >= 0 else 1e30, -w, -float(n_tr)], dtype=torch.float64, device=dev)
+                    dist.all_reduce(v, op=dist.ReduceOp.MIN)
+                    f, w = float(v[0].item()), -float(v[1].item())
+                    f = -1.0 if f >= 1e29 else f
+                    nt = torch.tensor([n_tr], dtype=torch.int64, device=dev)
+                    dist.all_reduce(nt)
+                    n_tr = int(nt.item())
+                ttfp.append(f)
+                wall.append(w)
+                tracked.append(n_tr)
+            found = bool(ra.found.item())
+            key = "inflight_stop" if inflight else "reference_semantics"
+            abort_info[key] = {
+                "found": found,
+                "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3) if found else None,
+                "kernel_exit_wall_ms": round(float(np.median(wall)) * 1e3, 3),
+                "paths_tracked": int(np.median(tracked))}
+        abort_info["note"] = ("device clock (s_memrealtime, rate from hipDeviceAttributeWallClockRate) from the "
+                              "first chunk's start, min over ranks; wall = host time to the all-GPU sync, max "
+                              "over ranks.  reference_semantics: paths in flight when the pose is found run to "
+                              "completion (..._TrunRANSAC.cu:148-152); inflight_stop: they stop at their next "
+                              "step boundary (hcAbortArgs::inflight_stop)")
 
     noisy_info = None
     if args.noisy_trials > 0:
@@ -228,7 +254,9 @@ def main():
 
     if rank == 0:
         med_launch_s = float(np.median(launch_ms)) / 1e3
-        achieved_tf = flops / med_launch_s / 1e12
+        achieved_tf = flops_exec / med_launch_s / 1e12
+        achieved_dense_tf = flops / med_launch_s / 1e12
+        traffic, traffic_src = traffic_bytes(TRACK_KERNEL)
         line = {
             "metric": "HC paths/sec (312 tracks x RANSAC samples)",
             "value": round(value, 1),
@@ -246,23 +274,40 @@ def main():
                                    "Abort_RANSAC=false",
                        "samples_per_gpu": S, "tracks_per_sample": 312, "paths_per_step": paths,
                        "streams": NS,
+                       "step": "reset tracks + one tracking launch; steps serialised on one stream, each a "
+                               "launch -> sync of one RANSAC batch (the reference's timer scope, "
+                               "GPU_HC_Solver.cpp:384,446)" if NS == 1 else
+                               f"reset tracks + one tracking launch, steps rotating over {NS} streams",
                        "single_launch_paths_per_s": round(paths / (float(np.median(launch_ms)) / 1e3), 1),
+                       "pipelined_paths_per_s": None if pipelined is None else round(pipelined, 1),
+                       "pipelined_streams": args.pipelined_streams if pipelined is not None else None,
+                       "pipelined_note": "the same K steps with consecutive batches overlapped on "
+                                         f"{args.pipelined_streams} streams (own buffers each): a batch's "
+                                         "tail runs beside the next batch's start; not the headline",
                        "parallelism": f"samples sharded over {world} GPU(s), no data-path collective",
                        "GPUHC_Max_Steps": tr.settings.max_steps,
                        "GPUHC_Max_Correction_Steps": tr.settings.max_corrections,
                        "kernel": _abi.lib().hc_trifocal_version().decode()},
-            "roofline": {"bound": "mfma", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
+            "roofline": {"bound": "valu_fp32", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
-                         "traffic": traffic_bytes(_abi.lib().hc_trifocal_version().decode()),
-                         "traffic_unit": "HBM bytes per launch (rocprofv3 FETCH_SIZE x2 gfx950 correction + "
-                                         "WRITE_SIZE, committed profiles/*_pmc_summary.json of this kernel "
-                                         "version; algorithmic ~0.5 KB/path = 15.3 MB/launch)",
-                         "note": "FP32-compute (VALU) bound tracker kernel; MI355X FP32 vector peak == FP32 MFMA "
-                                 "peak (157.3 TF). achieved = algorithmic FLOPs of the executed stages "
-                                 "(SURVEY 8d: 104.3 kFLOP/predictor stage, 101.3 kFLOP/corrector stage) / median "
-                                 "launch time (HIP events on the launch stream)",
+                         "traffic": traffic,
+                         "traffic_source": traffic_src,
+                         "traffic_unit": "HBM bytes per launch of the same kernel (rocprofv3 FETCH_SIZE x2 gfx950 "
+                                         "correction + WRITE_SIZE, separate --pmc passes, scripts/profile.sh); "
+                                         "algorithmic ~0.5 KB/path = 15.3 MB/launch",
+                         "achieved_dense_lu": round(achieved_dense_tf, 3),
+                         "frac_dense_lu": round(achieved_dense_tf / FP32_PEAK_TFLOPS, 4),
+                         "note": "FP32 VALU-issue/latency bound tracker kernel (no GEMM: 30x30 complex LUs of "
+                                 "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = FLOPs of "
+                                 "the executed stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 kFLOP / "
+                                 "corrector stage, with the LU's rank-1 updates counted over the column groups "
+                                 "the structurally sparse LU executes: 0.586 of the dense 68.4 kFLOP, "
+                                 "profiles/r2d_lu_work.json) / median single-launch kernel time (HIP events on "
+                                 "the launch stream). achieved_dense_lu prices the LU as the reference's dense "
+                                 "algorithm.",
                          "kernel_ms": round(float(np.median(launch_ms)), 4),
-                         "algorithmic_gflop_per_launch": round(flops / 1e9, 3),
+                         "executed_gflop_per_launch": round(flops_exec / 1e9, 3),
+                         "dense_lu_gflop_per_launch": round(flops / 1e9, 3),
                          "rk4_steps": steps_sum, "corrections": corr_sum},
             "solutions": {"converged": counts[0], "real": counts[1], "infinity": counts[2]},
             "pose": {"pose_support_ms": round(pose_ms, 4), "candidates": merged["num_candidates"],
@@ -278,7 +323,7 @@ def main():
         if abort_info is not None:
             line["early_abort"] = abort_info
         if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(problem, data, args.cpu_samples, value)
+            line["cpu_baseline"] = cpu_baseline(problem, data, args.cpu_samples, args.cpu_samples_4t, value)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -342,37 +387,89 @@ def noisy_pose_leg(args, tr, problem, data, world, rank, dev, stream):
             "median_candidates": int(np.median(cands))}
 
 
-def traffic_bytes(version):
-    """HBM bytes per tracker launch from the newest committed PMC summary of
-    this kernel version (PMC counters cannot be collected inside the timed run)."""
+def traffic_bytes(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (PMC counters cannot be collected inside the timed run): (bytes, file)."""
     import glob
-    best = None
+    best, src = None, None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
         try:
             with open(f) as fh:
                 d = json.load(fh)
         except (OSError, ValueError):
             continue
-        if d.get("version") == version and "hbm_bytes_per_launch" in d.get("derived", {}):
-            best = d["derived"]["hbm_bytes_per_launch"]
-    return best
+        if d.get("kernel") == kernel and "hbm_bytes_per_launch" in d.get("derived", {}):
+            best, src = d["derived"]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
+    return best, src
 
 
-def cpu_baseline(problem, data, n_samples, gpu_value):
-    """The oracle's CPU-HC restatement (CPUHC_Generic_Solver_Eval_by_Indx semantics,
-    OpenMP dynamic over paths) timed on this host's cores on a bounded sample."""
+def cpu_info():
+    """Host CPU model, logical CPUs and physical cores (/proc/cpuinfo)."""
+    model, phys = None, set()
+    try:
+        cur = {}
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if ":" not in line:
+                    if cur:
+                        phys.add((cur.get("physical id"), cur.get("core id")))
+                    cur = {}
+                    continue
+                k, v = (x.strip() for x in line.split(":", 1))
+                cur[k] = v
+                if k == "model name" and model is None:
+                    model = v
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    return model, os.cpu_count(), len(phys) or None
+
+
+def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
+    """CPU baselines on this host's cores, bounded samples of the config-2 workload:
+      value        the oracle's CPU-HC restatement (CPUHC_Generic_Solver_Eval_by_Indx
+                   semantics: no path pruning, LAPACK-style cgesv, OpenMP dynamic
+                   over paths) on the threads this job may use (OMP_NUM_THREADS,
+                   16 per GPU on the GPU box; capped by the host's cores);
+      threads4     the same on 4 threads (the reference's Num_Of_Cores default,
+                   gpuhc_settings.yaml:34);
+      pruned       the oracle's GPU-semantics tracker (depth-sign pruning, the work
+                   the GPU does) on the same threads: the apples-to-apples ratio."""
     from oracle import oracle as O
     from trifocal_pose_estimation_using_improved_gpuhc_amd import prepare_target_params
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    tgt, dif, _ = prepare_target_params(problem, data, seed=0, num_samples=n_samples)
-    s = O.settings(threads=threads)
-    _, _, _, _, secs = O.cpuhc_track(problem.start_sols, problem.start_params, tgt, dif,
-                                     problem.dHdx_index, problem.dHdt_index, s)
-    v = 312 * n_samples / secs
+    model, logical, physical = cpu_info()
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
+    threads = max(1, min(share, physical or logical or 1))
+    tgt, dif, _ = prepare_target_params(problem, data, seed=0, num_samples=max(n_samples, n_samples_4t))
+
+    def run(n, th):
+        _, _, _, _, secs = O.cpuhc_track(problem.start_sols, problem.start_params, tgt[:n], dif[:n],
+                                         problem.dHdx_index, problem.dHdt_index, O.settings(threads=th))
+        return 312 * n / secs, secs
+    v, secs = run(n_samples, threads)
+    v4, secs4 = run(n_samples_4t, 4)
+    t0 = time.perf_counter()
+    O.gpuhc_track(problem.start_sols, problem.start_params, tgt[:n_samples], dif[:n_samples], problem.unified_index,
+                  O.settings(threads=threads))
+    secs_p = time.perf_counter() - t0
+    vp = 312 * n_samples / secs_p
     return {"value": round(v, 1), "unit": "paths/s", "cores": threads, "kind": "port",
             "sample": f"CPU-HC restatement (oracle/hc_oracle.c orc_cpuhc_track, no path pruning, LAPACK-style "
-                      f"cgesv) on samples 0..{n_samples - 1} ({312 * n_samples} paths), {secs:.1f} s wall",
-            "gpu_over_cpu": round(gpu_value / v, 1)}
+                      f"cgesv) on config-2 samples 0..{n_samples - 1} ({312 * n_samples} paths), {secs:.1f} s "
+                      f"wall on {threads} threads",
+            "cpu_model": model, "host_logical_cpus": logical, "host_physical_cores": physical,
+            "threads_note": "threads = this job's CPU share (OMP_NUM_THREADS; the GPU box allots 16 per GPU), "
+                            "capped by the physical cores",
+            "threads4": {"value": round(v4, 1), "cores": 4, "samples": n_samples_4t, "seconds": round(secs4, 2),
+                         "note": "Num_Of_Cores default of gpuhc_settings.yaml:34"},
+            "pruned_gpu_semantics": {"value": round(vp, 1), "cores": threads, "samples": n_samples,
+                                     "seconds": round(secs_p, 2),
+                                     "note": "oracle orc_gpuhc_track: the GPU kernel's semantics (depth-sign "
+                                             "pruning) on the same threads"},
+            "gpu_over_cpu": round(gpu_value / v, 1),
+            "gpu_over_cpu_pruned": round(gpu_value / vp, 1),
+            "gpu_over_cpu_4threads": round(gpu_value / v4, 1)}
 
 
 if __name__ == "__main__":

@@ -1,0 +1,177 @@
+// hc_trifocal_shim.cpp -- drop-in replacement of the reference's four GPU-HC
+// launchers (magmaHC/gpu-kernels/magmaHC-kernels.hpp:24-105, implemented in
+// kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths[_TrunRANSAC][_Volta].cu)
+// on top of this repository's C-ABI (include/hc_trifocal.h).
+//
+// A maintainer compiles this file in place of the four .cu files and links
+// -lhc_trifocal; GPU_HC_Solver::Solve_by_GPU_HC (GPU_HC_Solver.cpp:390-436)
+// then runs unchanged.  Semantics kept from the reference:
+//  * C++ linkage, MAGMA types, the reference's parameter order;
+//  * the reference's pointer arrays (d_startSols_array: one pointer per track,
+//    d_Track_array: one per (sample, track)) are passed through as-is;
+//  * bool flags (1 byte) are the ABI's uint8_t flags;
+//  * the launch is asynchronous on the queue's stream and the return value is
+//    0.0 (..._TrunPaths.cu:385); failures are printed like the reference
+//    (:383), never exit();
+//  * abort mode uses the reference's semantics: paths in flight when a good
+//    hypothesis is found run to completion (hcAbortArgs::inflight_stop = 0);
+//  * the Volta variants take separate dH/dx and dH/dt tables: the shim
+//    concatenates them into the unified layout (Data_Reader.cpp:167-189) on the
+//    queue's stream before the launch.
+// The ABI never allocates on the hot path; the shim owns one workspace (and one
+// unified-table buffer for the Volta variants) per (device, stream), created on
+// first use and kept for the process lifetime.
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <utility>
+
+#include "hc_trifocal.h"
+#include "magmaHC-kernels.hpp"
+
+namespace {
+
+constexpr int kHxInts = 36000, kHtInts = 2880;   // dHdx_Index_Matrix_Size, dHdt_Index_Matrix_Size (..._TrunPaths.cu:311-320)
+
+struct StreamState {
+    void *workspace = nullptr;
+    int32_t *unified = nullptr;   // Volta variants only
+};
+
+StreamState *state_for(hipStream_t s, bool need_unified) {
+    static std::mutex mu;
+    static std::map<std::pair<int, hipStream_t>, StreamState> states;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    StreamState &st = states[{dev, s}];
+    if (!st.workspace && hipMalloc(&st.workspace, hc_trifocal_workspace_size()) != hipSuccess) st.workspace = nullptr;
+    if (need_unified && !st.unified &&
+        hipMalloc(reinterpret_cast<void **>(&st.unified), (kHxInts + kHtInts) * sizeof(int32_t)) != hipSuccess)
+        st.unified = nullptr;
+    if (!st.workspace || (need_unified && !st.unified)) return nullptr;
+    return &st;
+}
+
+hcTrackArgs make_args(int sub_RANSAC_iters, int max_steps, int max_corr, int inc_steps,
+                      magmaFloatComplex **d_startSols_array, magmaFloatComplex **d_Track_array,
+                      magmaFloatComplex *d_startParams, magmaFloatComplex *d_targetParams,
+                      magmaFloatComplex *d_diffParams, const int *d_unified, bool *d_conv, bool *d_inf) {
+    hcTrackArgs a{};
+    a.sub_ransac_iters = sub_RANSAC_iters;
+    a.settings.max_steps = max_steps;
+    a.settings.max_corrections = max_corr;
+    a.settings.delta_t_inc_steps = inc_steps;
+    a.start_sols_array = reinterpret_cast<const hcComplex *const *>(d_startSols_array);
+    a.track_array = reinterpret_cast<hcComplex *const *>(d_Track_array);
+    a.start_params = reinterpret_cast<const hcComplex *>(d_startParams);
+    a.target_params = reinterpret_cast<const hcComplex *>(d_targetParams);
+    a.diff_params = reinterpret_cast<const hcComplex *>(d_diffParams);
+    a.unified_index = reinterpret_cast<const int32_t *>(d_unified);
+    a.converge = reinterpret_cast<uint8_t *>(d_conv);
+    a.infinity = reinterpret_cast<uint8_t *>(d_inf);
+    return a;
+}
+
+void report(hcStatus st, const char *what) {
+    if (st != HC_SUCCESS) printf("%s failed: status %d (%s)\n", what, (int)st, hc_last_error_string());
+}
+
+const int32_t *unify(StreamState *st, const int *d_dHdx_indx, const int *d_dHdt_indx, hipStream_t s) {
+    if (hipMemcpyAsync(st->unified, d_dHdx_indx, kHxInts * sizeof(int32_t), hipMemcpyDeviceToDevice, s) != hipSuccess ||
+        hipMemcpyAsync(st->unified + kHxInts, d_dHdt_indx, kHtInts * sizeof(int32_t), hipMemcpyDeviceToDevice, s) !=
+            hipSuccess)
+        return nullptr;
+    return st->unified;
+}
+
+real_Double_t track(magma_queue_t q, int N, int max_steps, int max_corr, int inc_steps, magmaFloatComplex **ss,
+                    magmaFloatComplex **tracks, magmaFloatComplex *sp, magmaFloatComplex *tp, magmaFloatComplex *dp,
+                    const int *unified, const int *d_hx, const int *d_ht, bool *conv, bool *inf, const char *name) {
+    hipStream_t s = magma_queue_get_hip_stream(q);
+    StreamState *st = state_for(s, unified == nullptr);
+    if (!st) { report(HC_ERROR_WORKSPACE, name); return 0.0; }
+    const int32_t *U = unified ? reinterpret_cast<const int32_t *>(unified) : unify(st, d_hx, d_ht, s);
+    if (!U) { report(HC_ERROR_LAUNCH, name); return 0.0; }
+    hcTrackArgs a = make_args(N, max_steps, max_corr, inc_steps, ss, tracks, sp, tp, dp, U, conv, inf);
+    report(hc_trifocal_2op1p_30x30_track(&a, st->workspace, hc_trifocal_workspace_size(), (hcStream)s), name);
+    return 0.0;
+}
+
+real_Double_t track_abort(magma_queue_t q, int N, int E, int max_steps, int max_corr, int inc_steps,
+                          magmaFloatComplex **ss, magmaFloatComplex **tracks, magmaFloatComplex *sp,
+                          magmaFloatComplex *tp, magmaFloatComplex *dp, const int *unified, const int *d_hx,
+                          const int *d_ht, float *edgels, float *K, bool *conv, bool *inf, bool *found,
+                          int *batch_index, const char *name) {
+    hipStream_t s = magma_queue_get_hip_stream(q);
+    StreamState *st = state_for(s, unified == nullptr);
+    if (!st) { report(HC_ERROR_WORKSPACE, name); return 0.0; }
+    const int32_t *U = unified ? reinterpret_cast<const int32_t *>(unified) : unify(st, d_hx, d_ht, s);
+    if (!U) { report(HC_ERROR_LAUNCH, name); return 0.0; }
+    hcTrackArgs a = make_args(N, max_steps, max_corr, inc_steps, ss, tracks, sp, tp, dp, U, conv, inf);
+    hcAbortArgs ab{};
+    ab.num_triplet_edgels = E;
+    ab.triplet_edge_locations = edgels;
+    ab.intrinsic_matrix = K;
+    ab.found_trifocal_sols = reinterpret_cast<uint8_t *>(found);
+    ab.trifocal_sols_batch_index = batch_index;
+    ab.inflight_stop = 0;   // the reference's semantics (..._TrunRANSAC.cu:148-152)
+    report(hc_trifocal_2op1p_30x30_track_abort(&a, &ab, st->workspace, hc_trifocal_workspace_size(), (hcStream)s),
+           name);
+    return 0.0;
+}
+
+}  // namespace
+
+real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths(
+    magma_queue_t my_queue, int sub_RANSAC_iters, int HC_max_steps, int HC_max_correction_steps,
+    int HC_delta_t_incremental_steps, magmaFloatComplex **d_startSols_array, magmaFloatComplex **d_Track_array,
+    magmaFloatComplex *d_startParams, magmaFloatComplex *d_targetParams, magmaFloatComplex *d_diffParams,
+    int *d_unified_dHdx_dHdt_Index, bool *d_is_GPU_HC_Sol_Converge, bool *d_is_GPU_HC_Sol_Infinity,
+    magmaFloatComplex * /*d_Debug_Purpose*/) {
+    return track(my_queue, sub_RANSAC_iters, HC_max_steps, HC_max_correction_steps, HC_delta_t_incremental_steps,
+                 d_startSols_array, d_Track_array, d_startParams, d_targetParams, d_diffParams,
+                 d_unified_dHdx_dHdt_Index, nullptr, nullptr, d_is_GPU_HC_Sol_Converge, d_is_GPU_HC_Sol_Infinity,
+                 "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths");
+}
+
+real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_Volta(
+    magma_queue_t my_queue, int sub_RANSAC_iters, int HC_max_steps, int HC_max_correction_steps,
+    int HC_delta_t_incremental_steps, magmaFloatComplex **d_startSols_array, magmaFloatComplex **d_Track_array,
+    magmaFloatComplex *d_startParams, magmaFloatComplex *d_targetParams, magmaFloatComplex *d_diffParams,
+    int *d_dHdx_indx, int *d_dHdt_indx, bool *d_is_GPU_HC_Sol_Converge, bool *d_is_GPU_HC_Sol_Infinity,
+    magmaFloatComplex * /*d_Debug_Purpose*/) {
+    return track(my_queue, sub_RANSAC_iters, HC_max_steps, HC_max_correction_steps, HC_delta_t_incremental_steps,
+                 d_startSols_array, d_Track_array, d_startParams, d_targetParams, d_diffParams, nullptr, d_dHdx_indx,
+                 d_dHdt_indx, d_is_GPU_HC_Sol_Converge, d_is_GPU_HC_Sol_Infinity,
+                 "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_Volta");
+}
+
+real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_TrunRANSAC(
+    magma_queue_t my_queue, int sub_RANSAC_iters, int Num_Of_Triplet_Edgels, int HC_max_steps,
+    int HC_max_correction_steps, int HC_delta_t_incremental_steps, magmaFloatComplex **d_startSols_array,
+    magmaFloatComplex **d_Track_array, magmaFloatComplex *d_startParams, magmaFloatComplex *d_targetParams,
+    magmaFloatComplex *d_diffParams, int *d_unified_dHdx_dHdt_Index, float *d_Triplet_Edge_Locations,
+    float *d_Intrinsic_Matrix, bool *d_is_GPU_HC_Sol_Converge, bool *d_is_GPU_HC_Sol_Infinity,
+    magmaFloatComplex * /*d_Debug_Purpose*/, bool *d_Found_Trifocal_Sols, int *d_Trifocal_Sols_Batch_Index) {
+    return track_abort(my_queue, sub_RANSAC_iters, Num_Of_Triplet_Edgels, HC_max_steps, HC_max_correction_steps,
+                       HC_delta_t_incremental_steps, d_startSols_array, d_Track_array, d_startParams, d_targetParams,
+                       d_diffParams, d_unified_dHdx_dHdt_Index, nullptr, nullptr, d_Triplet_Edge_Locations,
+                       d_Intrinsic_Matrix, d_is_GPU_HC_Sol_Converge, d_is_GPU_HC_Sol_Infinity,
+                       d_Found_Trifocal_Sols, d_Trifocal_Sols_Batch_Index,
+                       "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_TrunRANSAC");
+}
+
+real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_TrunRANSAC_Volta(
+    magma_queue_t my_queue, int sub_RANSAC_iters, int Num_Of_Triplet_Edgels, int HC_max_steps,
+    int HC_max_correction_steps, int HC_delta_t_incremental_steps, magmaFloatComplex **d_startSols_array,
+    magmaFloatComplex **d_Track_array, magmaFloatComplex *d_startParams, magmaFloatComplex *d_targetParams,
+    magmaFloatComplex *d_diffParams, int *d_dHdx_indx, int *d_dHdt_indx, float *d_Triplet_Edge_Locations,
+    float *d_Intrinsic_Matrix, bool *d_is_GPU_HC_Sol_Converge, bool *d_is_GPU_HC_Sol_Infinity,
+    magmaFloatComplex * /*d_Debug_Purpose*/, bool *d_Found_Trifocal_Sols, int *d_Trifocal_Sols_Batch_Index) {
+    return track_abort(my_queue, sub_RANSAC_iters, Num_Of_Triplet_Edgels, HC_max_steps, HC_max_correction_steps,
+                       HC_delta_t_incremental_steps, d_startSols_array, d_Track_array, d_startParams, d_targetParams,
+                       d_diffParams, nullptr, d_dHdx_indx, d_dHdt_indx, d_Triplet_Edge_Locations, d_Intrinsic_Matrix,
+                       d_is_GPU_HC_Sol_Converge, d_is_GPU_HC_Sol_Infinity, d_Found_Trifocal_Sols,
+                       d_Trifocal_Sols_Batch_Index, "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths_TrunRANSAC_Volta");
+}

@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Executed LU work of the tracker (GPU only, development tool).
+
+Needs the HC_DIAG_LUWORK build (scripts/build_variant.sh luwork -DHC_DIAG_LUWORK,
+loaded through HC_TRIFOCAL_LIB): every LU solve adds the rank-1 update
+elements it executes (columns of the executed column groups x lanes of active
+path slots below the pivot).  The dense algorithm (the reference's) updates
+sum_{I} (29 - I)^2 = 8555 elements per solve; the structurally sparse LU skips
+column groups that are zero in both pivot rows of a wave.  Prints the executed
+fraction for one config-2 launch; bench.py prices the LU's update FLOPs with it.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi, load_problem, load_ransac_data, prepare_target_params  # noqa
+from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker  # noqa
+
+DENSE_UPDATE_ELEMENTS = sum((29 - i) ** 2 for i in range(30))   # 8555
+
+
+def main():
+    L = _abi.lib()
+    fn = L.hc_diag_luwork
+    fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    out = (C.c_ulonglong * 2)()
+    dev = torch.device("cuda:0")
+    problem = load_problem()
+    tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, 100)
+    tr = DeviceTracker(problem, dev)
+    r = tr.allocate(100)
+    tr.reset_tracks(r)
+    torch.cuda.synchronize()
+    fn(out, 1)
+    tr.launch(torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev), r)
+    torch.cuda.synchronize()
+    fn(out, 1)
+    st = r.stats.cpu().numpy()
+    stages = 4 * int(st[:, 0].sum()) + int(st[:, 1].sum())
+    elems, solves = int(out[0]), int(out[1])
+    res = {"config": "config 2 (100 samples, abort off), one launch",
+           "solves_counted": solves, "path_stages": stages,
+           "executed_update_elements": elems,
+           "executed_update_elements_per_solve": elems / max(1, solves),
+           "dense_update_elements_per_solve": DENSE_UPDATE_ELEMENTS,
+           "executed_fraction": elems / max(1, solves) / DENSE_UPDATE_ELEMENTS}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

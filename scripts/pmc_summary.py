@@ -41,7 +41,10 @@ if "SQ_WAVES" in c:
     der["cycles_per_wave"] = cyc
     der["eff_clock_ghz"] = cyc / out["avg_ns"]
     simds = 256 * 4
-    der["valu_issue_busy"] = c["SQ_INSTS_VALU"] / simds * 4 / cyc      # wave64 VALU = 4 cycles/instr
+    # SQ_ACTIVE_INST_* count quad-cycles (MI355X_MICROARCH.md): VALU-active cycles per SIMD / kernel cycles
+    if "SQ_ACTIVE_INST_VALU" in c:
+        der["valu_active_frac"] = c["SQ_ACTIVE_INST_VALU"] * 4 / simds / cyc
+        der["valu_active_cycles_per_inst"] = c["SQ_ACTIVE_INST_VALU"] * 4 / c["SQ_INSTS_VALU"]
     der["valu_per_wave"] = c["SQ_INSTS_VALU"] / waves
     der["lds_per_wave"] = c["SQ_INSTS_LDS"] / waves
     der["frac_wait_inst_any"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
@@ -58,6 +61,19 @@ if "WRITE_SIZE" in c:
     der["hbm_write_bytes"] = c["WRITE_SIZE"] * 1024
 if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     der["hbm_bytes_per_launch"] = der["hbm_fetch_bytes_corrected"] + der["hbm_write_bytes"]
+# FLOPs of the same bench run (its JSON line in the trace log): FLOP per VALU instruction
+try:
+    lines = [l for l in open(os.path.join(base, f"{tag}_trace.log")) if l.startswith("{")]
+    rl = json.loads(lines[-1])["roofline"]
+    if "SQ_INSTS_VALU" in c:
+        ex = rl.get("executed_gflop_per_launch")
+        de = rl.get("dense_lu_gflop_per_launch", rl.get("algorithmic_gflop_per_launch"))
+        if ex:
+            der["flop_per_valu_executed"] = ex * 1e9 / c["SQ_INSTS_VALU"]
+        if de:
+            der["flop_per_valu_dense_lu"] = de * 1e9 / c["SQ_INSTS_VALU"]
+except (OSError, ValueError, KeyError, IndexError):
+    pass
 out["derived"] = der
 s = json.dumps(out, indent=1)
 print(s)

@@ -473,7 +473,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         eval_hx(rA, s_hx, map, S, r_v);                                      // :184 / :220
         wave_lds_sync();
         HC_DIAG_MARK(2);
+#ifdef HC_DIAG_LUWORK
+        const cf k = lu_solve(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent), __ballot(act));
+#else
         const cf k = lu_solve(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));   // :188 / :224
+#endif
         wave_lds_sync();
         HC_DIAG_MARK(5);
         {
@@ -568,7 +572,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restric
         if (rA[c].x != 0.0f || rA[c].y != 0.0f) pat |= 1u << c;   // NaN counts as non-zero
     }
     const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
-    const cf x = lu_solve(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)]);
+    const cf x = lu_solve(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)], __ballot(sys < n));
     if (ok) X[(size_t)sys * NV + r] = x;
 }
 
@@ -724,6 +728,17 @@ int hc_diag_phases(unsigned long long *out, int reset) {
     if (reset) {
         static const unsigned long long z[13] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_phase), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+#ifdef HC_DIAG_LUWORK
+int hc_diag_luwork(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_luwork), sizeof(unsigned long long) * 2) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[2] = {0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_luwork), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
 }

@@ -174,14 +174,30 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, LUB
     }
 }
 
+#ifdef HC_DIAG_LUWORK
+// diagnostic build: rank-1 update elements the solves execute (sum over the
+// executed column groups of columns x active lanes), and the solves
+__device__ unsigned long long g_diag_luwork[2];
+struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work counts (active path slots)
+#define HC_LU_WORK(ncols) (lu_work_acc.acc += (unsigned long long)(ncols) * \
+    (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask))
+#else
+#define HC_LU_WORK(ncols) do { } while (0)
+#endif
+
 // a_j -= l * u_j for the groups K.. of step I (the caller is inside the
 // below-the-pivot exec region)
 template <int I, int K>
-__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, const LUBuf &L) {
+__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, const LUBuf &L
+#ifdef HC_DIAG_LUWORK
+                                          , LuWork &lu_work_acc
+#endif
+) {
     using C = LuChunks<LU_CHUNK>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
         if (pmw & C::mask(I, K)) {
+            HC_LU_WORK(N);
             cf u[N];
             if constexpr (N == 1) {
                 u[0] = L.row[J];
@@ -196,13 +212,21 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        lu_update<I, K + 1>(rA, l, pmw, L);
+        lu_update<I, K + 1>(rA, l, pmw, L
+#ifdef HC_DIAG_LUWORK
+                            , lu_work_acc
+#endif
+        );
     }
 }
 
 template <int I>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool all_dense, int lane,
-                                           int r, int hb, bool row_lane, PivF &my, LUBuf &L) {
+                                           int r, int hb, bool row_lane, PivF &my, LUBuf &L
+#ifdef HC_DIAG_LUWORK
+                                           , LuWork &lu_work_acc
+#endif
+) {
     if constexpr (I < NV) {
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
         const bool elig = rowid >= I && row_lane;
@@ -289,9 +313,17 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
             pat |= (((pat >> I) & 1u) != 0u || dense) ? pmwd : 0u;
-            lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, L);
+            lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, L
+#ifdef HC_DIAG_LUWORK
+                            , lu_work_acc
+#endif
+            );
         }
-        lu_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+        lu_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L
+#ifdef HC_DIAG_LUWORK
+                          , lu_work_acc
+#endif
+        );
     }
 }
 
@@ -323,7 +355,9 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 // Solves the system of each half: lane r holds row r of A in rA and b_r in
 // rB; pattern = the structural pattern of row r.  Returns x_r in lane r.  L is
 // this half's buffer (16-B aligned).
-__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L) {
+__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L,
+                                      unsigned long long count_mask = ~0ull) {
+    (void)count_mask;   // diagnostic builds (HC_DIAG_LUWORK): lanes whose executed work is counted
     // every entry finite and below 2^88 in magnitude (NaN fails the compare)
     bool ok = true;
 #pragma unroll
@@ -335,7 +369,17 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     int rowid = row_lane ? r : 99;   // padding lanes never pivot
     uint32_t pat = row_lane ? pattern : 0u;
     PivF my{pf2{0.0f, 0.0f}};
+#ifdef HC_DIAG_LUWORK
+    LuWork lu_work_acc{0ull, count_mask};
+    lu_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L, lu_work_acc);
+    const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
+    if (lane == 0) {
+        atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
+        atomicAdd(&g_diag_luwork[1], solves);
+    }
+#else
     lu_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+#endif
     lu_backward<NV - 1>(rA, rB, rowid, my, hb);
     // lane r returns x_r: the owner of position r holds it in rB
     wave_lds_sync();
