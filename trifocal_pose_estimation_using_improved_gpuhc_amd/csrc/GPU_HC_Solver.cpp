@@ -77,7 +77,7 @@ bool HC_Settings::b(const std::string &k, bool dflt) const {
 
 // ------------------------------------------------------------------ per-GPU state
 struct GPU_HC_Solver::PerGPU {
-    int dev = 0, N = 0;
+    int dev = 0, g = 0, N = 0;   // HIP device, logical GPU index (== dev unless Share_Devices)
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hcComplex *d_Start_Sols = nullptr, *d_Track = nullptr, *d_Start_Params = nullptr;
@@ -126,14 +126,20 @@ GPU_HC_Solver::GPU_HC_Solver(const HC_Settings &S, const std::string &root_dir) 
     // check_multiGPUs (GPU_HC_Solver.hpp:175-193), reported as exceptions instead of exit(1)
     if (Num_Of_GPUs < 1 || Num_Of_GPUs > MAX_NUM_OF_GPUS)
         throw std::runtime_error("Num_Of_GPUs must be in [1, " + std::to_string(MAX_NUM_OF_GPUS) + "]");
-    if (Num_Of_GPUs > device_count) throw std::runtime_error("Not enough GPUs");
+    // Share_Devices (not in the reference): more logical GPUs than devices, logical
+    // GPU g on device g % device_count with its own stream and buffers -- the
+    // multi-GPU split, launch loop and result stacking on a single-GPU machine
+    const bool share = S.b("Share_Devices", false);
+    if (Num_Of_GPUs > device_count && !share) throw std::runtime_error("Not enough GPUs");
+    if (device_count < 1) throw std::runtime_error("no GPU");
     hc_split_samples(Num_Of_RANSAC_Iterations, Num_Of_GPUs, sub_RANSAC_iters);   // :85-88
     for (int g = 0; g < Num_Of_GPUs; g++) {
         printf("GPU %2d computes %2d RANSAC iterations\n", g, sub_RANSAC_iters[g]);
         auto *p = new PerGPU();
-        p->dev = g;
+        p->g = g;
+        p->dev = g % device_count;
         p->N = sub_RANSAC_iters[g];
-        HC_HIP_CHECK(hipSetDevice(g));
+        HC_HIP_CHECK(hipSetDevice(p->dev));
         HC_HIP_CHECK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
         HC_HIP_CHECK(hipEventCreate(&p->ev0));
         HC_HIP_CHECK(hipEventCreate(&p->ev1));
@@ -294,7 +300,7 @@ void GPU_HC_Solver::Data_Transfer_From_Host_To_Device() {
             HC_HIP_CHECK(hipMemsetAsync(p->d_found, 0, 1, p->stream));
         }
         HC_HIP_CHECK(hipStreamSynchronize(p->stream));
-        transfer_h2d_time[p->dev] = now_s() - t0;
+        transfer_h2d_time[p->g] = now_s() - t0;
         offset += p->N;
     }
 }
@@ -388,7 +394,7 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
         HC_HIP_CHECK(hipSetDevice(p->dev));
         float ms = 0.0f;
         HC_HIP_CHECK(hipEventElapsedTime(&ms, p->ev0, p->ev1));
-        gpu_time[p->dev] = ms / 1e3;
+        gpu_time[p->g] = ms / 1e3;
         const double t0 = now_s();
         const size_t n = (size_t)NT * p->N;
         if (n) {
@@ -405,9 +411,9 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
                                        hipMemcpyDeviceToHost));
             double ff = -1.0;
             hc_trifocal_read_timings(p->d_ws, &ff);
-            first_good_pose_time[p->dev] = ff;
+            first_good_pose_time[p->g] = ff;
         }
-        transfer_d2h_time[p->dev] = now_s() - t0;
+        transfer_d2h_time[p->g] = now_s() - t0;
         h_GPU_HC_Track_Sols_Stack.insert(h_GPU_HC_Track_Sols_Stack.end(), p->h_track.begin(), p->h_track.end());
         h_is_GPU_HC_Sol_Converge_Stack.insert(h_is_GPU_HC_Sol_Converge_Stack.end(), p->h_conv.begin(), p->h_conv.end());
         h_is_GPU_HC_Sol_Infinity_Stack.insert(h_is_GPU_HC_Sol_Infinity_Stack.end(), p->h_inf.begin(), p->h_inf.end());
@@ -470,8 +476,8 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
         int g = 0;
         for (PerGPU *p : gpus_) {
             std::cout << "GPU id " << p->dev << " found solution? " << (h_Found_Stack[g] ? "Yes" : "No");
-            if (h_Found_Stack[g] && first_good_pose_time[p->dev] >= 0)
-                printf(" (first good pose after %.3f ms on device)", first_good_pose_time[p->dev] * 1e3);
+            if (h_Found_Stack[g] && first_good_pose_time[p->g] >= 0)
+                printf(" (first good pose after %.3f ms on device)", first_good_pose_time[p->g] * 1e3);
             std::cout << std::endl;
             g++;
         }

@@ -27,6 +27,7 @@ static void usage() {
            "  -g, --gpus        number of GPUs (overrides Num_Of_GPUs)\n"
            "  -t, --times       test rounds (TEST_RANSAC_TIMES, default 1)\n"
            "      --abort       Abort_RANSAC_by_Good_Sol = true\n"
+           "      --share-devices  allow more GPUs (-g) than devices: logical GPU g runs on device g %% count\n"
            "      --inflight-stop  abort mode: paths in flight also stop once a pose is found\n"
            "                    (Abort_Inflight_Stop; default: they run to completion as in the reference)\n"
            "      --write-sols  write Output_Write_Files/GPU_Converged_HC_tracks.txt\n"
@@ -37,7 +38,7 @@ static void usage() {
 int main(int argc, char **argv) {
     std::string problem, root = "../../";
     int samples = -1, gpus = -1, times = 1;
-    bool abort_flag = false, write_sols = false, quirks = false, inflight_stop = false;
+    bool abort_flag = false, write_sols = false, quirks = false, inflight_stop = false, share = false;
     std::string dataset;
     if (argc <= 1) { usage(); return 0; }
     for (int i = 1; i < argc; i++) {
@@ -54,6 +55,7 @@ int main(int argc, char **argv) {
         else if (a == "-t" || a == "--times") times = std::stoi(next("-t"));
         else if (a == "--abort") abort_flag = true;
         else if (a == "--inflight-stop") inflight_stop = true;
+        else if (a == "--share-devices") share = true;
         else if (a == "--write-sols") write_sols = true;
         else if (a == "--quirks") quirks = true;
         else if (a == "-s" || a == "--dataset") dataset = next("-s");
@@ -71,6 +73,7 @@ int main(int argc, char **argv) {
         if (gpus > 0) s.set("Num_Of_GPUs", std::to_string(gpus));
         if (abort_flag) s.set("Abort_RANSAC_by_Good_Sol", "true");
         if (inflight_stop) s.set("Abort_Inflight_Stop", "true");
+        if (share) s.set("Share_Devices", "true");
         if (write_sols) s.set("Write_Converged_Sols", "true");
         if (quirks) s.set("Pose_Selection_Reference_Quirks", "true");
         if (!dataset.empty()) s.set("RANSAC_Dataset", dataset);
