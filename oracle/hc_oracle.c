@@ -34,6 +34,16 @@ static inline cf cadd(cf a, cf b) { return cmk(a.x + b.x, a.y + b.y); }
 static inline cf csub(cf a, cf b) { return cmk(a.x - b.x, a.y - b.y); }
 static inline cf cscale(cf a, float s) { return cmk(a.x * s, a.y * s); }
 static inline cf cdivs(cf a, float s) { return cmk(a.x / s, a.y / s); }
+#ifdef ORC_PLAIN_OPS
+/* Experiment build only (libhc_oracle_plain.so, scripts/cpuhc_pin.py): the
+   reference's host operators as plain expressions (MAGMA magma_operators.h
+   order), compiled like the reference CPU build (g++ -O3 -march=native, GCC's
+   default -ffp-contract=fast, CMakeLists.txt:36,57), so the compiler chooses
+   the FMAs as it did for CPU_HC_Solver. */
+static inline cf cmul(cf a, cf b) { return cmk(a.x * b.x - a.y * b.y, a.y * b.x + a.x * b.y); }
+static inline cf cmadd(cf acc, cf a, cf b) { return cadd(acc, cmul(a, b)); }
+static inline cf cmsub(cf acc, cf a, cf b) { return csub(acc, cmul(a, b)); }
+#else
 /* a*b with the two documented FMAs */
 static inline cf cmul(cf a, cf b) {
     return cmk(fmaf(a.x, b.x, -(a.y * b.y)), fmaf(a.x, b.y, a.y * b.x));
@@ -46,6 +56,7 @@ static inline cf cmadd(cf acc, cf a, cf b) {
 static inline cf cmsub(cf acc, cf a, cf b) {
     return cmk(fmaf(a.y, b.y, fmaf(-a.x, b.x, acc.x)), fmaf(-a.y, b.x, fmaf(-a.x, b.y, acc.y)));
 }
+#endif
 /* MAGMA_C_DIV == cuCdivf (CUDA cuComplex.h), literal, no FMA */
 static inline cf cdiv(cf a, cf b) {
     float s = fabsf(b.x) + fabsf(b.y);
@@ -765,9 +776,11 @@ void orc_add_pixel_noise(int E, const float *loc, const float *K, double sigma, 
 
 /* ====================================================================== */
 /* LAPACK cgesv semantics (call sites CPUHC_Generic_Solver_Eval_by_Indx.cpp:93,100,107,114,127) */
-/* cgetf2 (right-looking, icamax on cabs1, first max) + cgetrs.  The       */
-/* OpenBLAS 0.3.23 kernels the reference links are not reproducible here:  */
-/* PARITY UNPINNED beyond the aggregate CPU counts.    */
+/* cgetf2 (right-looking, icamax on cabs1, first max) + cgetrs: the test  */
+/* build's LU.  The reference links OpenBLAS 0.3.23, whose kernels differ  */
+/* in FMA use; orc_set_external_cgesv routes the CPU-HC solves through that */
+/* library (scripts/cpuhc_pin.py), which with the plain-operator build     */
+/* reproduces CPU_Sols_Statistics.txt exactly (tests/test_oracle_kat.py).  */
 /* ====================================================================== */
 static int cgesv_lapack(cf *A /* col-major 30x30 */, cf *B) {
     int ipiv[NV], info = 0;
@@ -815,6 +828,24 @@ int orc_cgesv_lapack(float *Af, float *Bf) {
     return info;
 }
 
+
+/* Experiment hook (scripts/cpuhc_pin.py only): route the CPU-HC solves through
+   an external LAPACK cgesv with the ILP64 interface (OpenBLAS `cgesv_64_`),
+   the library the reference links (CPUHC_Generic_Solver_Eval_by_Indx.cpp:93). */
+typedef void (*orc_ext_cgesv64)(const long long *n, const long long *nrhs, void *A, const long long *lda,
+                                long long *ipiv, void *B, const long long *ldb, long long *info);
+static orc_ext_cgesv64 g_ext_cgesv = 0;
+void orc_set_external_cgesv(void *fn) { g_ext_cgesv = (orc_ext_cgesv64)fn; }
+static inline void cpu_lu(cf *A, cf *B) {
+    if (g_ext_cgesv) {
+        const long long n = NV, nrhs = 1, ld = NV;
+        long long ipiv[NV], info = 0;
+        g_ext_cgesv(&n, &nrhs, A, &ld, ipiv, B, &ld, &info);
+        return;
+    }
+    cgesv_lapack(A, B);
+}
+
 /* ====================================================================== */
 /* CPU-HC -- cpuhc-solvers/CPUHC_Generic_Solver_Eval_by_Indx.cpp:22-251     */
 /* cpu-jacobian-evals/cpu-eval-indx_trifocal_2op1p_30x30.hpp:22-89 (column-major A) */
@@ -850,7 +881,7 @@ static void cpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
         const float h2 = (float)(0.5 * (double)delta_t);                  /* :84 */
         nsteps++;
         /* (i) :90-94 + k2 helper :180-191 */
-        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cgesv_lapack(A, B);
+        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cpu_lu(A, B);
         for (int i = 0; i < NV; i++) {
             inter[i] = cadd(inter[i], cdivs(cscale(cscale(B[i], delta_t), 1.0f), 6.0f));
             B[i] = cscale(B[i], h2);
@@ -858,7 +889,7 @@ static void cpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
         }
         t0 += h2;
         /* (ii) :97-101 + k3 helper :193-205 */
-        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cgesv_lapack(A, B);
+        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cpu_lu(A, B);
         for (int i = 0; i < NV; i++) {
             inter[i] = cadd(inter[i], cdivs(cscale(cscale(B[i], delta_t), 1.0f), 3.0f));
             x[i] = last[i];
@@ -866,7 +897,7 @@ static void cpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
             x[i] = cadd(x[i], B[i]);
         }
         /* (iii) :104-108 + k4 helper :207-220 */
-        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cgesv_lapack(A, B);
+        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cpu_lu(A, B);
         for (int i = 0; i < NV; i++) {
             inter[i] = cadd(inter[i], cdivs(cscale(cscale(B[i], delta_t), 1.0f), 3.0f));
             x[i] = last[i];
@@ -875,7 +906,7 @@ static void cpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
         }
         t0 += h2;
         /* (iv) :111-117 + prediction :222-230 */
-        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cgesv_lapack(A, B);
+        param_homotopy_cpu(t0, spf, tpp, p); EVAL_HX(); EVAL_HT(); cpu_lu(A, B);
         for (int i = 0; i < NV; i++) {
             inter[i] = cadd(inter[i], cdivs(cscale(cscale(B[i], delta_t), 1.0f), 6.0f));
             x[i] = inter[i];
@@ -883,7 +914,7 @@ static void cpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
         for (int c = 0; c < s->max_corrections; c++) {                    /* :122-135 */
             EVAL_HX();
             for (int r = 0; r < NV; r++) B[r] = h_row(dHdt, r, x, p);
-            cgesv_lapack(A, B);
+            cpu_lu(A, B);
             ncorr++;
             float sq_sols = 0.0f, sq_corr = 0.0f;                         /* :232-251 */
             for (int i = 0; i < NV; i++) {

@@ -115,6 +115,11 @@ double orc_cpuhc_track(const orc_hc_settings *s, int num_samples,
                        const int *dHdx, const int *dHdt,
                        float *tracks, uint8_t *conv, uint8_t *inf, orc_path_stats *stats);
 
+/* Route orc_cpuhc_track's solves through an external ILP64 LAPACK cgesv
+   (OpenBLAS `cgesv_64_`; NULL restores the restated getf2/getrs).  Pin
+   experiments only (scripts/cpuhc_pin.py). */
+void orc_set_external_cgesv(void *cgesv64);
+
 /* Evaluations::Evaluate_HC_Sols counts over 312*N paths:
    out[0] converged, out[1] real (all 30 |Im| <= 1e-4 among converged), out[2] inf. */
 void orc_count_solutions(int num_samples, const float *tracks, const uint8_t *conv,
