@@ -35,7 +35,7 @@ static inline cf csub(cf a, cf b) { return cmk(a.x - b.x, a.y - b.y); }
 static inline cf cscale(cf a, float s) { return cmk(a.x * s, a.y * s); }
 static inline cf cdivs(cf a, float s) { return cmk(a.x / s, a.y / s); }
 #ifdef ORC_PLAIN_OPS
-/* Experiment build only (libhc_oracle_plain.so, scripts/cpuhc_pin.py): the
+/* Experiment build only (libhc_oracle_plain.so, tests/cpuhc_pin.py): the
    reference's host operators as plain expressions (MAGMA magma_operators.h
    order), compiled like the reference CPU build (g++ -O3 -march=native, GCC's
    default -ffp-contract=fast, CMakeLists.txt:36,57), so the compiler chooses
@@ -779,7 +779,7 @@ void orc_add_pixel_noise(int E, const float *loc, const float *K, double sigma, 
 /* cgetf2 (right-looking, icamax on cabs1, first max) + cgetrs: the test  */
 /* build's LU.  The reference links OpenBLAS 0.3.23, whose kernels differ  */
 /* in FMA use; orc_set_external_cgesv routes the CPU-HC solves through that */
-/* library (scripts/cpuhc_pin.py), which with the plain-operator build     */
+/* library (tests/cpuhc_pin.py), which with the plain-operator build     */
 /* reproduces CPU_Sols_Statistics.txt exactly (tests/test_oracle_kat.py).  */
 /* ====================================================================== */
 static int cgesv_lapack(cf *A /* col-major 30x30 */, cf *B) {
@@ -829,7 +829,7 @@ int orc_cgesv_lapack(float *Af, float *Bf) {
 }
 
 
-/* Experiment hook (scripts/cpuhc_pin.py only): route the CPU-HC solves through
+/* Experiment hook (tests/cpuhc_pin.py only): route the CPU-HC solves through
    an external LAPACK cgesv with the ILP64 interface (OpenBLAS `cgesv_64_`),
    the library the reference links (CPUHC_Generic_Solver_Eval_by_Indx.cpp:93). */
 typedef void (*orc_ext_cgesv64)(const long long *n, const long long *nrhs, void *A, const long long *lda,

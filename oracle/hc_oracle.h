@@ -117,7 +117,7 @@ double orc_cpuhc_track(const orc_hc_settings *s, int num_samples,
 
 /* Route orc_cpuhc_track's solves through an external ILP64 LAPACK cgesv
    (OpenBLAS `cgesv_64_`; NULL restores the restated getf2/getrs).  Pin
-   experiments only (scripts/cpuhc_pin.py). */
+   experiments only (tests/cpuhc_pin.py). */
 void orc_set_external_cgesv(void *cgesv64);
 
 /* Evaluations::Evaluate_HC_Sols counts over 312*N paths:

@@ -7,7 +7,7 @@ trifocal_pose_estimation_using_improved_gpuhc_amd/ and never imports oracle/.
 Parity status: pinned by reference-data KATs (H(start)=0, Hx = FD(H)), numpy
 LU, and the reference's committed CPU-HC counts, reproduced EXACTLY
 (11098 / 521 / 6577) by the restatement built like the reference CPU build and
-solving through OpenBLAS 0.3.23 (tests/test_oracle_kat.py, scripts/cpuhc_pin.py);
+solving through OpenBLAS 0.3.23 (tests/test_oracle_kat.py, tests/cpuhc_pin.py);
 the reference sources are never built or run here (SURVEY.md §8c denial,
 binding).  See DESIGN.md §5.
 """

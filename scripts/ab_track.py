@@ -19,11 +19,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def child(samples):
     sys.path.insert(0, ROOT)
-    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     import numpy as np
     import torch
 
-    from make_golden import track_hash
+    def track_hash(tracks):   # the golden fixture's per-path hash (tests/golden/make_golden.py)
+        a = np.ascontiguousarray(tracks[:, :30, :], np.float32).copy()
+        a[a == 0] = 0.0
+        a[np.isnan(a)] = np.float32(np.nan)
+        w = a.reshape(a.shape[0], -1).view(np.uint32).astype(np.uint64)
+        h = np.zeros(a.shape[0], np.uint64)
+        with np.errstate(over="ignore"):
+            for k in range(w.shape[1]):
+                h = (h * np.uint64(1099511628211)) ^ w[:, k]
+        return h
     from trifocal_pose_estimation_using_improved_gpuhc_amd import load_problem, load_ransac_data, prepare_target_params
     from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker
     dev = torch.device("cuda:0")

@@ -13,8 +13,8 @@ Variables tried (each in its own process):
          openblas:<CORE> : OpenBLAS 0.3.23.dev `cgesv_64_` (the version the
                  reference links), kernel set forced with OPENBLAS_CORETYPE.
 
-Test/experiment infrastructure only; writes one JSON line per variant.
-    python scripts/cpuhc_pin.py [--samples 100] [--out profiles/r2_cpuhc_pin.json]
+Test infrastructure only (tests/ may load the oracle); writes one JSON line per variant.
+    python tests/cpuhc_pin.py [--samples 100] [--out profiles/r2_cpuhc_pin.json]
 """
 import ctypes as C
 import json

@@ -92,6 +92,22 @@ def noisy_fixture(ss, sp, U, loc, tan, K):
           "candidates", sel["num_candidates"], "paths", sel["path21"], sel["path31"], "residuals", res, ok)
 
 
+def heldout_fixture(ss, sp, U):
+    """Per-path tracking cost (4 * RK4 steps + corrections, GPU-HC semantics) on
+    the two synthcurves datasets the benchmark does NOT use (Triplet_Edgels_001,
+    _002; srand(0), 100 samples each): the input of scripts/make_track_order.py,
+    so the tracker's dequeue order is not fitted on the benchmark workload."""
+    costs = []
+    for ds in ("001", "002"):
+        loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", f"Triplet_Edgels_{ds}.txt"))
+        tgt, dif, _ = O.prepare_target_params(0, [100], loc, tan, sp)
+        _, _, _, st = O.gpuhc_track(ss, sp, tgt, dif, U)
+        costs.append((4 * st["steps"].astype(np.int32) + st["corrections"].astype(np.int32)).reshape(100, 312))
+    np.savez_compressed(os.path.join(HERE, "track_cost_heldout.npz"), cost=np.concatenate(costs).astype(np.int16),
+                        datasets=np.array(["001", "002"]))
+    print("held-out track costs", np.concatenate(costs).shape)
+
+
 def main():
     only = sys.argv[sys.argv.index("--only") + 1] if "--only" in sys.argv else None
     ss, sp, dhdx, dhdt = O.read_problem(PROB)
@@ -99,6 +115,9 @@ def main():
     loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", "Triplet_Edgels_000.txt"))
     K = O.read_floats(os.path.join(RANS, "Intrinsic_Matrix.txt"), 9)
     tgt, dif, picked = O.prepare_target_params(0, [100], loc, tan, sp)
+    if only == "heldout":
+        heldout_fixture(ss, sp, U)
+        return
     if only == "pose":
         tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
         pose_fixture(tr, conv, loc, K)

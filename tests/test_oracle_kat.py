@@ -161,7 +161,7 @@ def test_kat4_cpuhc_counts_exact_with_reference_build_and_openblas():
     with its Haswell kernels.  profiles/r2_cpuhc_pin.json has the sweep (spec
     vs plain operators x restated LU vs OpenBLAS Haswell / SkylakeX / Zen /
     Sandybridge kernels): only plain + Haswell and plain + Zen are exact.
-    Runs scripts/cpuhc_pin.py's child in its own process (OPENBLAS_CORETYPE
+    Runs tests/cpuhc_pin.py's child in its own process (OPENBLAS_CORETYPE
     must be set before the library loads); about 45 s on 8 threads."""
     import json
     import subprocess
@@ -169,7 +169,7 @@ def test_kat4_cpuhc_counts_exact_with_reference_build_and_openblas():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OPENBLAS_CORETYPE="Haswell")
     subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "all", "plain"], check=True)
-    p = subprocess.run([sys.executable, os.path.join(root, "scripts", "cpuhc_pin.py"), "--child", "plain",
+    p = subprocess.run([sys.executable, os.path.join(root, "tests", "cpuhc_pin.py"), "--child", "plain",
                         "openblas:Haswell", "100"], env=env, capture_output=True, text=True, timeout=900)
     assert p.returncode == 0, p.stderr[-2000:]
     res = json.loads(p.stdout.strip().splitlines()[-1])

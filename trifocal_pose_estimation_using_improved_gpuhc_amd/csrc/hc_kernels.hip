@@ -15,6 +15,9 @@
 // paths on the device and raises an agent-scope flag.
 #include "hc_device.hpp"
 #include "hc_lu.hpp"
+#ifdef HC_CGESV4
+#include "hc_lu4.hpp"
+#endif
 #include "../../include/hc_trifocal.h"
 
 #include <cstdlib>
@@ -35,7 +38,11 @@ static inline hcStatus launch_status(hcStatus on_fail) {
 // queue position q -> track c_track_order[q / N], sample q % N.  Results are
 // per batch id, so the order only changes when a path runs, not what it computes.
 __constant__ int c_track_order[NTRK] = {
+#ifdef HC_AB_TRACK_ORDER
+#include HC_AB_TRACK_ORDER
+#else
 #include "hc_track_order.inc"
+#endif
 };
 __device__ __forceinline__ int path_of_queue_pos(int q, int num_paths, int ordered) {
     if (!ordered) return q;
@@ -576,6 +583,39 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restric
     if (ok) X[(size_t)sys * NV + r] = x;
 }
 
+#ifdef HC_CGESV4
+// Experiment build only (-DHC_CGESV4, scripts/lu_ab.py): the LU
+// with four systems per wave (hc_lu4.hpp), lane q of group g holds rows q, q + 16.
+// Bit-identical, 27 % slower than k_cgesv (3 waves/SIMD instead of 5).
+__global__ void __launch_bounds__(WG_THREADS) k_cgesv4(int n, const cf *__restrict__ A, const cf *__restrict__ B,
+                                                       cf *__restrict__ X) {
+    __shared__ LUBuf4 s_lu[4 * WAVES_PER_WG];
+    const int lane = lane_id();
+    const int q = lane & 15, g = lane >> 4, w = threadIdx.x / WAVE;
+    const int sys0 = (blockIdx.x * WAVES_PER_WG + w) * 4;
+    const int sys = sys0 + g;
+    const bool ok = sys < n, r1ok = q < NV - 16;
+    cf a0[NV], a1[NV];
+    uint32_t p0 = 0, p1 = 0;
+#pragma unroll
+    for (int c = 0; c < NV; c++) {
+        a0[c] = ok ? A[((size_t)sys * NV + q) * NV + c] : cmk(0.0f, 0.0f);
+        a1[c] = (ok && r1ok) ? A[((size_t)sys * NV + q + 16) * NV + c] : cmk(0.0f, 0.0f);
+        if (a0[c].x != 0.0f || a0[c].y != 0.0f) p0 |= 1u << c;   // NaN counts as non-zero
+        if (a1[c].x != 0.0f || a1[c].y != 0.0f) p1 |= 1u << c;
+    }
+    const cf b0 = ok ? B[(size_t)sys * NV + q] : cmk(0.0f, 0.0f);
+    const cf b1 = (ok && r1ok) ? B[(size_t)sys * NV + q + 16] : cmk(0.0f, 0.0f);
+    unsigned act = 0u;
+#pragma unroll
+    for (int k = 0; k < 4; k++) act |= (sys0 + k < n) ? 1u << k : 0u;
+    cf x0, x1;
+    lu_solve4(a0, a1, b0, b1, lane, p0, p1, act, s_lu[w * 4 + g], x0, x1);
+    if (ok) X[(size_t)sys * NV + q] = x0;
+    if (ok && r1ok) X[(size_t)sys * NV + q + 16] = x1;
+}
+#endif
+
 // dH/dx, dH/dt, H at n points: one point per half-wave
 __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws, const cf *__restrict__ X,
                                                      const cf *__restrict__ P, const cf *__restrict__ D,
@@ -671,6 +711,9 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.num_paths = (int)paths;
     // abort mode dequeues sample-major, so whole hypotheses finish as early as possible
     k.ordered = abort_mode ? 0 : 1;
+#ifdef HC_AB_NATURAL_ORDER
+    k.ordered = 0;
+#endif
     k.max_steps = t->settings.max_steps;
     k.max_corr = t->settings.max_corrections;
     k.inc_steps = t->settings.delta_t_inc_steps;
@@ -789,9 +832,15 @@ hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, h
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
     (void)hipGetLastError();
+#ifdef HC_CGESV4
+    const int per = 4 * hc::WAVES_PER_WG;
+    hipLaunchKernelGGL(hc::k_cgesv4, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
+                       (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+#else
     const int per = 2 * hc::WAVES_PER_WG;
     hipLaunchKernelGGL(hc::k_cgesv, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
                        (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
+#endif
     return hc::launch_status(HC_ERROR_LAUNCH);
 }
 
