@@ -51,6 +51,7 @@ __device__ __forceinline__ int path_of_queue_pos(int q, int num_paths, int order
     return (q - rank * n) * NTRK + c_track_order[rank];
 }
 
+constexpr int PRIO_TENTHS = 10;   // issue-priority levels over the queue (k_track)
 constexpr int WG_THREADS = 256;
 constexpr int WAVES_PER_WG = WG_THREADS / WAVE;
 
@@ -282,6 +283,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 
     // per-slot state (uniform within a half)
     int ph = PH_DEQ, b = -1, smp_loaded = -1;
+    int qpos = 0;   // queue position of the slot's path (issue priority)
     unsigned found_seen = 0u;   // abort mode: the found flag as of the last stage
 #ifdef HC_DIAG_TIMES
     int diag_t0 = 0;
@@ -345,6 +347,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     b = -1;
                 } else {
                     b = path_of_queue_pos(nb, a.num_paths, a.ordered);
+                    qpos = nb;
                     bool skip = false;
                     if (ABORT) {                                              // TrunRANSAC.cu:152
                         skip = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
@@ -424,6 +427,20 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
         }
         if (__ballot(ph == PH_STAGE) == 0ull) break;
+        if (!ABORT && a.ordered) {
+            // Issue priority by queue position (s_setprio, arbitration among the
+            // waves of a SIMD): the last tenth of the queue at 3, the tenth
+            // before at 2, the one before that at 1.  Paths dequeued late
+            // decide when the launch ends; the earlier ones have slack
+            // (profiles/r2_ab_priority.jsonl: -1.8 %).
+            const int qp = (ph == PH_STAGE) ? qpos : 0;
+            const int m = max(__builtin_amdgcn_readlane(qp, 0), __builtin_amdgcn_readlane(qp, 32));
+            const int lvl = (int)((long long)m * PRIO_TENTHS / a.num_paths);
+            if (lvl >= PRIO_TENTHS - 1) __builtin_amdgcn_s_setprio(3);
+            else if (lvl >= PRIO_TENTHS - 2) __builtin_amdgcn_s_setprio(2);
+            else if (lvl >= PRIO_TENTHS - 3) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         HC_DIAG_MARK(0);
         // the found flag for the next step boundary: read now, used after the stage
         if (ABORT && a.inflight_stop) found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -866,8 +883,8 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
 const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
-           "readlane back substitution, pipelined evals, 5 waves/SIMD)";
+    return "hc_trifocal gfx950 v9.1 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
+           "readlane back substitution, pipelined evals, 5 waves/SIMD, queue-position issue priority)";
 }
 
 }  // extern "C"
