@@ -163,6 +163,21 @@ def main():
     torch.cuda.synchronize(dev)
     launch_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
 
+    # ablation of the papers' path truncation: the same launch through
+    # the archived ..._PH_CodeOpt semantics (no depth-sign truncation), HIP events
+    ab_buf = tr.allocate(S, stats=True)
+    aev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+    for a_, b_ in aev:
+        tr.reset_tracks(ab_buf)
+        a_.record(stream)
+        tr.launch(tgt, dif, ab_buf, stream=stream, truncate=False)
+        b_.record(stream)
+    torch.cuda.synchronize(dev)
+    ph_ms = float(np.median([a_.elapsed_time(b_) for a_, b_ in aev]))
+    ph_host = ab_buf.host()
+    ph_stages = int(4 * ph_host["stats"]["steps"].astype(np.int64).sum() + ph_host["stats"]["corrections"].astype(np.int64).sum())
+    del ab_buf
+
     # device pose recovery + maximal support over the launch's tracks,
     # timed separately with HIP events on the same stream
     from trifocal_pose_estimation_using_improved_gpuhc_amd import pose as P
@@ -318,6 +333,16 @@ def main():
                              "candidate over all triplet edgels + maximal-support selection "
                              "(Evaluations.cpp:298-504), merged over ranks (RCCL all_gather)"},
         }
+        tp_ms = float(np.median(launch_ms))
+        line["ablation_trunpaths"] = {
+            "note": "the papers' path truncation by depth signs (..._TrunPaths.cu:148-155) on and off: the same "
+                    "config-2 launch through hc_trifocal_2op1p_30x30_track (TrunPaths) and "
+                    "hc_trifocal_2op1p_30x30_track_ph_codeopt (archived ..._PH_CodeOpt), single launch, HIP events",
+            "trunpaths": {"kernel_ms": round(tp_ms, 4), "paths_per_s": round(312 * S / (tp_ms / 1e3), 1),
+                          "stages": steps_sum * 4 + corr_sum},
+            "ph_codeopt": {"kernel_ms": round(ph_ms, 4), "paths_per_s": round(312 * S / (ph_ms / 1e3), 1),
+                           "stages": ph_stages},
+            "speedup": round(ph_ms / tp_ms, 3)}
         if noisy_info is not None:
             line["noisy_pose"] = noisy_info
         if abort_info is not None:

@@ -126,6 +126,16 @@ hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAb
                                              void *workspace, size_t workspace_bytes,
                                              hcStream stream);
 
+/* GPU-HC tracking WITHOUT the depth-sign path truncation: every path runs
+   until it converges, diverges or reaches the step limit.  Replaces the
+   archived ablation launchers kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt and
+   ..._PH_CodeOpt_Volta (arxived_GPU_code/gpu-kernels/magmaHC-kernels.hpp:61-96),
+   whose kernel is ..._TrunPaths without ..._TrunPaths.cu:148-155 (the archived
+   kernel files differ in exactly those lines).  Same arguments and outputs as
+   hc_trifocal_2op1p_30x30_track. */
+hcStatus hc_trifocal_2op1p_30x30_track_ph_codeopt(const hcTrackArgs *args, void *workspace,
+                                                  size_t workspace_bytes, hcStream stream);
+
 /* HC_SUCCESS, or HC_ERROR_TABLE when the last launch on this workspace found
    an index table that does not fit the kernels' compaction (the tracker then
    left every output untouched).  Blocking read -- call after synchronising. */

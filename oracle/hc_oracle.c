@@ -363,7 +363,7 @@ static void gpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
 
     int succ = 0;                                     /* sipiv[30], :123 */
     float t0 = 0.0f, t_step = 0.0f, delta_t = 0.01f;  /* :80 */
-    int end_zone = 0, check_depths = 1;
+    int end_zone = 0, check_depths = s->no_truncation ? 0 : 1;   /* 0: archived ..._PH_CodeOpt.cu */
     int isSucc = 0, isInf = 0;
     int nsteps = 0, ncorr = 0;
     float vs[NV], vc[NV];

@@ -264,3 +264,20 @@ def test_residual_gate_on_golden_candidates(problem):
     assert len(worst) == int(g["num_candidates"]) and max(worst) <= RESIDUAL_TOL
     best = int(np.nonzero(g["cand_ids"] == g["path"][0])[0][0])
     assert worst[best] < 1e-5
+
+
+def test_truncation_only_ends_paths_early():
+    """TrunPaths vs the archived PH_CodeOpt (golden runs of config 2): truncation
+    only stops paths early (..._TrunPaths.cu:148-155), so no path takes more steps
+    with it, and every path that converged or diverged under truncation was never
+    truncated and is identical without it (flags, steps, corrections, track)."""
+    t = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    p = np.load(os.path.join(GOLDEN, "gpuhc_phcodeopt_N100_seed0.npz"))
+    assert (t["steps"] <= p["steps"]).all()
+    ended = (t["conv"] == 1) | (t["inf"] == 1)
+    assert ended.sum() > 3000   # (a path can carry both flags: conv is read from t0 after an inf break)
+    for k in ("conv", "inf", "steps", "corrections", "hash"):
+        assert (t[k][ended] == p[k][ended]).all(), k
+    # what truncation saves: 31 % of the predictor + corrector stages of config 2
+    st = lambda g: int(4 * g["steps"].astype(np.int64).sum() + g["corrections"].astype(np.int64).sum())  # noqa: E731
+    assert 0.25 < 1 - st(t) / st(p) < 0.4

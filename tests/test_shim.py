@@ -2,8 +2,8 @@
 
 CPU: the shim compiles against the reference's launcher signatures
 (integration/magmaHC-kernels.hpp restating magmaHC-kernels.hpp:24-105, with a
-types-only MAGMA stand-in) and exports the four C++-linkage launchers with
-exactly those parameter lists.
+types-only MAGMA stand-in) and exports the four C++-linkage launchers (plus the two archived ..._PH_CodeOpt
+ablation launchers) with exactly those parameter lists.
 
 GPU: each of the four launchers, called with the reference's argument lists
 (pointer arrays d_startSols_array / d_Track_array as GPU_HC_Solver.cpp:352-353
@@ -34,6 +34,13 @@ SIGNATURES = {
         "(magma_queue*, int, int, int, int, int, magmaFloatComplex**, magmaFloatComplex**, magmaFloatComplex*, "
         "magmaFloatComplex*, magmaFloatComplex*, int*, int*, float*, float*, bool*, bool*, magmaFloatComplex*, "
         "bool*, int*)",
+    # archived ablation launchers (arxived_GPU_code/gpu-kernels/magmaHC-kernels.hpp:61-96)
+    "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt":
+        "(magma_queue*, int, int, int, int, magmaFloatComplex**, magmaFloatComplex**, magmaFloatComplex*, "
+        "magmaFloatComplex*, magmaFloatComplex*, int*, bool*, bool*, magmaFloatComplex*)",
+    "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_Volta":
+        "(magma_queue*, int, int, int, int, magmaFloatComplex**, magmaFloatComplex**, magmaFloatComplex*, "
+        "magmaFloatComplex*, magmaFloatComplex*, int*, int*, bool*, bool*, magmaFloatComplex*)",
 }
 
 
@@ -52,21 +59,24 @@ def _lib():
     L.shim_queue_create.restype = C.c_void_p
     L.shim_queue_create.argtypes = [C.c_void_p]
     L.shim_queue_destroy.argtypes = [C.c_void_p]
-    for f in ("shim_trunpaths", "shim_trunpaths_volta", "shim_trunransac", "shim_trunransac_volta"):
+    for f in ("shim_trunpaths", "shim_trunpaths_volta", "shim_trunransac", "shim_trunransac_volta",
+              "shim_ph_codeopt", "shim_ph_codeopt_volta"):
         getattr(L, f).restype = C.c_double
     return L
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("abort", [False, True])
+@pytest.mark.parametrize("abort,truncate", [(False, True), (True, True), (False, False)])
 @pytest.mark.parametrize("volta", [False, True])
-def test_shim_launchers_match_abi(problem, samples100, tracker, ransac0, abort, volta):
+def test_shim_launchers_match_abi(problem, samples100, tracker, ransac0, abort, truncate, volta):
+    """truncate=False: the archived ..._PH_CodeOpt[_Volta] launchers against
+    hc_trifocal_2op1p_30x30_track_ph_codeopt."""
     import torch
     L = _lib()
     dev = tracker.device
     N = 3
     tgt, dif, _ = samples100
-    ref = tracker.track(tgt[:N], dif[:N], abort=abort).host()
+    ref = tracker.track(tgt[:N], dif[:N], abort=abort, truncate=truncate).host()
     # the reference's device layout (GPU_HC_Solver.cpp:137-184,335-362): start sols and
     # tracks as 31-complex columns, addressed through per-track pointer arrays
     ss = torch.from_numpy(problem.start_sols).to(dev)
@@ -95,8 +105,11 @@ def test_shim_launchers_match_abi(problem, samples100, tracker, ransac0, abort, 
         fn = L.shim_trunransac_volta if volta else L.shim_trunransac
         rv = fn(C.c_void_p(q), C.c_int(N), C.c_int(E.shape[0]), *common, *tables, p(E), p(tracker.K), p(conv), p(inf),
                 p(found), p(bidx))
-    else:
+    elif truncate:
         fn = L.shim_trunpaths_volta if volta else L.shim_trunpaths
+        rv = fn(C.c_void_p(q), C.c_int(N), *common, *tables, p(conv), p(inf))
+    else:
+        fn = L.shim_ph_codeopt_volta if volta else L.shim_ph_codeopt
         rv = fn(C.c_void_p(q), C.c_int(N), *common, *tables, p(conv), p(inf))
     torch.cuda.synchronize(dev)
     L.shim_queue_destroy(C.c_void_p(q))

@@ -73,6 +73,7 @@ static_assert(offsetof(Workspace, tab) == 64, "control block is 64 bytes");
 struct KArgs {
     int num_paths;
     int ordered;        // dequeue track-major in c_track_order (abort mode off)
+    int truncate;       // depth-sign path truncation (..._TrunPaths.cu:148-155); 0 = PH_CodeOpt
     int max_steps, max_corr, inc_steps;
     const cf *start_sols;
     const cf *const *start_sols_array;
@@ -379,7 +380,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         sols = rl ? dstart[r] : cmk(0.0f, 0.0f);
                         xl = x;
                         t0 = 0.0f; t_step = 0.0f; dt = 0.01f;                 // :80
-                        end_zone = false; check = true; isSucc = false; isInf = false;
+                        end_zone = false; check = a.truncate != 0; isSucc = false; isInf = false;
                         succ = 0; nsteps = 0; ncorr = 0; stepidx = 0;
                         ph = PH_BEGIN;
                     }
@@ -703,7 +704,7 @@ static int grid_for(int waves_needed, const void *kernel) {
 }
 
 static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *workspace, size_t wsb,
-                             hcStream stream, bool abort_mode) {
+                             hcStream stream, bool abort_mode, bool truncate = true) {
     if (!t || t->sub_ransac_iters < 0) return HC_ERROR_INVALID_VALUE;
     if (!workspace || wsb < ws_bytes_needed()) return HC_ERROR_WORKSPACE;
     if (t->sub_ransac_iters == 0) return HC_SUCCESS;
@@ -728,6 +729,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.num_paths = (int)paths;
     // abort mode dequeues sample-major, so whole hypotheses finish as early as possible
     k.ordered = abort_mode ? 0 : 1;
+    k.truncate = truncate ? 1 : 0;
 #ifdef HC_AB_NATURAL_ORDER
     k.ordered = 0;
 #endif
@@ -814,6 +816,11 @@ hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace,
 hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAbortArgs *abort_args,
                                              void *workspace, size_t workspace_bytes, hcStream stream) {
     return hc::launch_track(args, abort_args, workspace, workspace_bytes, stream, true);
+}
+
+hcStatus hc_trifocal_2op1p_30x30_track_ph_codeopt(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,
+                                                  hcStream stream) {
+    return hc::launch_track(args, nullptr, workspace, workspace_bytes, stream, false, false);
 }
 
 hcStatus hc_trifocal_workspace_status(const void *workspace) {

@@ -101,7 +101,8 @@ class DeviceTracker:
 
     def launch(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, abort: bool = False,
                stream: torch.cuda.Stream | None = None, workspace: torch.Tensor | None = None,
-               sample_offset: int = 0, num_samples: int | None = None, inflight_stop: bool = False) -> None:
+               sample_offset: int = 0, num_samples: int | None = None, inflight_stop: bool = False,
+               truncate: bool = True) -> None:
         """Enqueue one tracking run on `stream` (no synchronisation).
 
         Samples [sample_offset, sample_offset + num_samples) of `target`/`diff`
@@ -109,7 +110,8 @@ class DeviceTracker:
         launch's batch ids (abort-mode batch_index values) are local to it.
         inflight_stop (abort mode): paths in flight also stop once a pose is
         found (hcAbortArgs::inflight_stop; default: the reference's semantics,
-        they run to completion)."""
+        they run to completion).  truncate=False: no depth-sign path
+        truncation (the archived ..._PH_CodeOpt kernel, hc_trifocal_2op1p_30x30_track_ph_codeopt)."""
         if num_samples is None:
             num_samples = target.shape[0] - sample_offset
         if num_samples < 0 or sample_offset < 0 or sample_offset + num_samples > target.shape[0] or \
@@ -136,6 +138,8 @@ class DeviceTracker:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         hs = C.c_void_p(s.cuda_stream)
         ws = C.c_void_p(ws_t.data_ptr())
+        if abort and not truncate:
+            raise _abi.HCError("abort mode always truncates paths (..._TrunRANSAC.cu)")
         if abort:
             if self.edgels is None:
                 raise _abi.HCError("abort mode needs set_ransac_data() first")
@@ -148,6 +152,9 @@ class DeviceTracker:
             ab.inflight_stop = 1 if inflight_stop else 0
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track_abort")
+        elif not truncate:
+            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph_codeopt(C.byref(a), ws, self.ws_bytes, hs),
+                       "hc_trifocal_2op1p_30x30_track_ph_codeopt")
         else:
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track(C.byref(a), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track")
@@ -188,13 +195,13 @@ class DeviceTracker:
         return a.value, b.value, hz.value
 
     def track(self, target: np.ndarray, diff: np.ndarray, abort: bool = False, stats: bool = True,
-              inflight_stop: bool = False) -> TrackResult:
+              inflight_stop: bool = False, truncate: bool = True) -> TrackResult:
         """Synchronous convenience wrapper: H2D params, reset tracks, launch, sync, status check."""
         tgt = torch.from_numpy(np.ascontiguousarray(target, np.float32)).to(self.device)
         dif = torch.from_numpy(np.ascontiguousarray(diff, np.float32)).to(self.device)
         r = self.allocate(tgt.shape[0], stats=stats, abort=abort)
         self.reset_tracks(r)
-        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop)
+        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop, truncate=truncate)
         torch.cuda.synchronize(self.device)
         self.workspace_status()
         return r
