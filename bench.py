@@ -163,19 +163,23 @@ def main():
     torch.cuda.synchronize(dev)
     launch_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
 
-    # ablation of the papers' path truncation: the same launch through
-    # the archived ..._PH_CodeOpt semantics (no depth-sign truncation), HIP events
+    # the papers' ablation ladder: the same launch through the archived
+    # ..._PH (explicit RK, no truncation) and ..._PH_CodeOpt (no truncation) semantics
     ab_buf = tr.allocate(S, stats=True)
-    aev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
-    for a_, b_ in aev:
-        tr.reset_tracks(ab_buf)
-        a_.record(stream)
-        tr.launch(tgt, dif, ab_buf, stream=stream, truncate=False)
-        b_.record(stream)
-    torch.cuda.synchronize(dev)
-    ph_ms = float(np.median([a_.elapsed_time(b_) for a_, b_ in aev]))
-    ph_host = ab_buf.host()
-    ph_stages = int(4 * ph_host["stats"]["steps"].astype(np.int64).sum() + ph_host["stats"]["corrections"].astype(np.int64).sum())
+
+    def ablation(**kw):
+        aev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+        for a_, b_ in aev:
+            tr.reset_tracks(ab_buf)
+            a_.record(stream)
+            tr.launch(tgt, dif, ab_buf, stream=stream, truncate=False, **kw)
+            b_.record(stream)
+        torch.cuda.synchronize(dev)
+        h = ab_buf.host()
+        return (float(np.median([a_.elapsed_time(b_) for a_, b_ in aev])),
+                int(4 * h["stats"]["steps"].astype(np.int64).sum() + h["stats"]["corrections"].astype(np.int64).sum()))
+    ph_ms, ph_stages = ablation(explicit_rk=True)
+    phc_ms, phc_stages = ablation()
     del ab_buf
 
     # device pose recovery + maximal support over the launch's tracks,
@@ -334,15 +338,19 @@ def main():
                              "(Evaluations.cpp:298-504), merged over ranks (RCCL all_gather)"},
         }
         tp_ms = float(np.median(launch_ms))
-        line["ablation_trunpaths"] = {
-            "note": "the papers' path truncation by depth signs (..._TrunPaths.cu:148-155) on and off: the same "
-                    "config-2 launch through hc_trifocal_2op1p_30x30_track (TrunPaths) and "
-                    "hc_trifocal_2op1p_30x30_track_ph_codeopt (archived ..._PH_CodeOpt), single launch, HIP events",
-            "trunpaths": {"kernel_ms": round(tp_ms, 4), "paths_per_s": round(312 * S / (tp_ms / 1e3), 1),
-                          "stages": steps_sum * 4 + corr_sum},
-            "ph_codeopt": {"kernel_ms": round(ph_ms, 4), "paths_per_s": round(312 * S / (ph_ms / 1e3), 1),
-                           "stages": ph_stages},
-            "speedup": round(ph_ms / tp_ms, 3)}
+        leg = lambda ms, st: {"kernel_ms": round(ms, 4), "paths_per_s": round(312 * S / (ms / 1e3), 1),  # noqa: E731
+                              "stages": st}
+        line["ablation"] = {
+            "note": "the papers' incremental strategies on MI355X: the same config-2 launch (single launch, HIP "
+                    "events) through the archived ..._PH semantics (direct parameter homotopy, explicit RK "
+                    "helpers; hc_trifocal_2op1p_30x30_track_ph), ..._PH_CodeOpt (loopy RK; "
+                    "hc_trifocal_2op1p_30x30_track_ph_codeopt) and ..._PH_CodeOpt_TrunPaths (depth-sign path "
+                    "truncation, ..._TrunPaths.cu:148-155; the headline kernel).  P2C is not built: its "
+                    "parameter-to-coefficient generator is not in the reference",
+            "ph": leg(ph_ms, ph_stages),
+            "ph_codeopt": leg(phc_ms, phc_stages),
+            "ph_codeopt_trunpaths": leg(tp_ms, steps_sum * 4 + corr_sum),
+            "trunpaths_speedup_over_ph_codeopt": round(phc_ms / tp_ms, 3)}
         if noisy_info is not None:
             line["noisy_pose"] = noisy_info
         if abort_info is not None:

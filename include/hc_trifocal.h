@@ -136,6 +136,17 @@ hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAb
 hcStatus hc_trifocal_2op1p_30x30_track_ph_codeopt(const hcTrackArgs *args, void *workspace,
                                                   size_t workspace_bytes, hcStream stream);
 
+/* The archived ..._PH kernel (direct parameter homotopy, no code
+   optimisation): PH_CodeOpt with the explicit Runge-Kutta helpers of
+   magmaHC/dev-get-new-data.cuh:37-71 instead of the loopy RK, i.e. the stage
+   sums s += ((k*dt)*gc*1.0)/6 and /3 (a division, where the loopy RK multiplies
+   by the rounded 1/6 and 1/3) and x += k*((h/2 or h)*gc), gc = MAGMA_C_ONE.
+   Replaces kernel_GPUHC_trifocal_2op1p_30x30_PH
+   (arxived_GPU_code/gpu-kernels/magmaHC-kernels.hpp:42-59), which takes
+   separate dH/dx and dH/dt tables; here the unified table as everywhere. */
+hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspace,
+                                          size_t workspace_bytes, hcStream stream);
+
 /* HC_SUCCESS, or HC_ERROR_TABLE when the last launch on this workspace found
    an index table that does not fit the kernels' compaction (the tracker then
    left every output untouched).  Blocking read -- call after synchronising. */

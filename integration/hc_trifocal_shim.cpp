@@ -1,8 +1,9 @@
 // hc_trifocal_shim.cpp -- drop-in replacement of the reference's four GPU-HC
 // launchers (magmaHC/gpu-kernels/magmaHC-kernels.hpp:24-105, implemented in
 // kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths[_TrunRANSAC][_Volta].cu)
-// and of the two archived ablation launchers ..._PH_CodeOpt[_Volta]
-// (arxived_GPU_code/gpu-kernels/magmaHC-kernels.hpp:61-96: no path truncation)
+// and of the archived ablation launchers ..._PH_CodeOpt[_Volta] (no path
+// truncation) and ..._PH (explicit RK as well; arxived_GPU_code/gpu-kernels/
+// magmaHC-kernels.hpp:42-96)
 // on top of this repository's C-ABI (include/hc_trifocal.h).
 //
 // A maintainer compiles this file in place of the four .cu files and links
@@ -90,7 +91,7 @@ const int32_t *unify(StreamState *st, const int *d_dHdx_indx, const int *d_dHdt_
 real_Double_t track(magma_queue_t q, int N, int max_steps, int max_corr, int inc_steps, magmaFloatComplex **ss,
                     magmaFloatComplex **tracks, magmaFloatComplex *sp, magmaFloatComplex *tp, magmaFloatComplex *dp,
                     const int *unified, const int *d_hx, const int *d_ht, bool *conv, bool *inf, const char *name,
-                    bool truncate = true) {
+                    bool truncate = true, bool explicit_rk = false) {
     hipStream_t s = magma_queue_get_hip_stream(q);
     StreamState *st = state_for(s, unified == nullptr);
     if (!st) { report(HC_ERROR_WORKSPACE, name); return 0.0; }
@@ -98,8 +99,9 @@ real_Double_t track(magma_queue_t q, int N, int max_steps, int max_corr, int inc
     if (!U) { report(HC_ERROR_LAUNCH, name); return 0.0; }
     hcTrackArgs a = make_args(N, max_steps, max_corr, inc_steps, ss, tracks, sp, tp, dp, U, conv, inf);
     const size_t wsb = hc_trifocal_workspace_size();
-    report(truncate ? hc_trifocal_2op1p_30x30_track(&a, st->workspace, wsb, (hcStream)s)
-                    : hc_trifocal_2op1p_30x30_track_ph_codeopt(&a, st->workspace, wsb, (hcStream)s),
+    report(explicit_rk ? hc_trifocal_2op1p_30x30_track_ph(&a, st->workspace, wsb, (hcStream)s)
+           : truncate  ? hc_trifocal_2op1p_30x30_track(&a, st->workspace, wsb, (hcStream)s)
+                       : hc_trifocal_2op1p_30x30_track_ph_codeopt(&a, st->workspace, wsb, (hcStream)s),
            name);
     return 0.0;
 }
@@ -204,4 +206,16 @@ real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_Volta(
                  d_startSols_array, d_Track_array, d_startParams, d_targetParams, d_diffParams, nullptr, d_dHdx_indx,
                  d_dHdt_indx, d_is_GPU_HC_Sol_Converge, d_is_GPU_HC_Sol_Infinity,
                  "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_Volta", false);
+}
+
+real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH(
+    magma_queue_t my_queue, int sub_RANSAC_iters, int HC_max_steps, int HC_max_correction_steps,
+    int HC_delta_t_incremental_steps, magmaFloatComplex **d_startSols_array, magmaFloatComplex **d_Track_array,
+    magmaFloatComplex *d_startParams, magmaFloatComplex *d_targetParams, magmaFloatComplex *d_diffParams,
+    int *d_dHdx_indx, int *d_dHdt_indx, bool *d_is_GPU_HC_Sol_Converge, bool *d_is_GPU_HC_Sol_Infinity,
+    magmaFloatComplex * /*d_Debug_Purpose*/) {
+    return track(my_queue, sub_RANSAC_iters, HC_max_steps, HC_max_correction_steps, HC_delta_t_incremental_steps,
+                 d_startSols_array, d_Track_array, d_startParams, d_targetParams, d_diffParams, nullptr, d_dHdx_indx,
+                 d_dHdt_indx, d_is_GPU_HC_Sol_Converge, d_is_GPU_HC_Sol_Infinity,
+                 "kernel_GPUHC_trifocal_2op1p_30x30_PH", false, true);
 }

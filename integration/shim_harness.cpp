@@ -37,6 +37,11 @@ double shim_ph_codeopt_volta(void *q, int n, int ms, int mc, int inc, mfc **ssa,
     return kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_Volta(static_cast<magma_queue_t>(q), n, ms, mc, inc, ssa, tra,
                                                               sp, tp, dp, hx, ht, conv, inf, nullptr);
 }
+double shim_ph(void *q, int n, int ms, int mc, int inc, mfc **ssa, mfc **tra, mfc *sp, mfc *tp, mfc *dp, int *hx,
+               int *ht, bool *conv, bool *inf) {
+    return kernel_GPUHC_trifocal_2op1p_30x30_PH(static_cast<magma_queue_t>(q), n, ms, mc, inc, ssa, tra, sp, tp, dp, hx,
+                                                ht, conv, inf, nullptr);
+}
 double shim_trunransac(void *q, int n, int e, int ms, int mc, int inc, mfc **ssa, mfc **tra, mfc *sp, mfc *tp,
                        mfc *dp, int *unified, float *edgels, float *K, bool *conv, bool *inf, bool *found,
                        int *batch_index) {

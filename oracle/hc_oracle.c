@@ -395,7 +395,19 @@ static void gpuhc_one_path(const orc_hc_settings *s, int bid, const float *ssf, 
                 B[r] = ht_row(dHdt, r, x, p, dif);
             }
             cgesv_gpu(A, B, kk);                                          /* :188 */
-            if (rk < 3) {                                                 /* :191-205 */
+            if (rk < 3 && s->explicit_rk) {
+                /* archived ..._PH.cu with dev-get-new-data.cuh:37-71 (gc = MAGMA_C_ONE):
+                   s += ((k*dt)*gc*1.0)/(6|3); x = (rk ? x_last : x) + k*((h2|dt)*gc) */
+                const cf one = cmk(1.0f, 0.0f);
+                const float dv = rk == 0 ? 6.0f : 3.0f;
+                const cf g = cmk(rk == 2 ? delta_t : h2, 0.0f);
+                for (int r = 0; r < NV; r++) {
+                    sols[r] = cadd(sols[r], cdivs(cscale(cmul(cscale(kk[r], delta_t), one), 1.0f), dv));
+                    if (rk > 0) x[r] = xl[r];
+                    x[r] = cadd(x[r], cmul(kk[r], g));
+                }
+                if (rk != 1) t0 += h2;
+            } else if (rk < 3) {                                          /* :191-205 */
                 const float w = (float)((double)coef * 1.0 / 6.0);
                 for (int r = 0; r < NV; r++) {
                     sols[r] = cadd(sols[r], cscale(cscale(kk[r], delta_t), w));

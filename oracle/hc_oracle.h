@@ -74,6 +74,7 @@ typedef struct {
     int inc_steps;          /* GPUHC_Num_Of_Steps_to_Increase_Delta_t   */
     int num_threads;        /* OpenMP threads (<=0: runtime default)    */
     int no_truncation;      /* GPU-HC only: 1 = PH_CodeOpt, no depth-sign truncation */
+    int explicit_rk;        /* GPU-HC only: 1 = archived ..._PH RK arithmetic (dev-get-new-data.cuh) */
 } orc_hc_settings;
 
 /* Per-path statistics (same layout as hcPathStats in include/hc_trifocal.h). */

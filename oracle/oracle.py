@@ -28,7 +28,8 @@ HX_SIZE, HT_SIZE = 36000, 2880
 
 class Settings(C.Structure):
     _fields_ = [("max_steps", C.c_int), ("max_corrections", C.c_int),
-                ("inc_steps", C.c_int), ("num_threads", C.c_int), ("no_truncation", C.c_int)]
+                ("inc_steps", C.c_int), ("num_threads", C.c_int), ("no_truncation", C.c_int),
+                ("explicit_rk", C.c_int)]
 
 
 PATH_STATS_DTYPE = np.dtype([("steps", "<i4"), ("corrections", "<i4"),
@@ -55,8 +56,9 @@ def _p(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
-def settings(max_steps=80, max_corrections=3, inc_steps=4, threads=0, truncate=True) -> Settings:
-    return Settings(max_steps, max_corrections, inc_steps, threads, 0 if truncate else 1)
+def settings(max_steps=80, max_corrections=3, inc_steps=4, threads=0, truncate=True, explicit_rk=False) -> Settings:
+    """explicit_rk=True, truncate=False: the archived ..._PH kernel's semantics."""
+    return Settings(max_steps, max_corrections, inc_steps, threads, 0 if truncate else 1, 1 if explicit_rk else 0)
 
 
 # ----------------------------------------------------------------- readers

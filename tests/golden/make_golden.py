@@ -108,15 +108,17 @@ def heldout_fixture(ss, sp, U):
     print("held-out track costs", np.concatenate(costs).shape)
 
 
-def ph_codeopt_fixture(ss, sp, U, tgt, dif):
+def ph_codeopt_fixture(ss, sp, U, tgt, dif, explicit_rk=False):
     """Config 2 through the archived ..._PH_CodeOpt semantics (no depth-sign
-    truncation; the archived kernel is ..._TrunPaths without :148-155)."""
-    tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U, O.settings(truncate=False))
-    np.savez_compressed(os.path.join(HERE, "gpuhc_phcodeopt_N100_seed0.npz"),
+    truncation; the archived kernel is ..._TrunPaths without :148-155), or with
+    explicit_rk the archived ..._PH semantics (explicit RK helpers as well)."""
+    tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U, O.settings(truncate=False, explicit_rk=explicit_rk))
+    name = "gpuhc_ph_N100_seed0.npz" if explicit_rk else "gpuhc_phcodeopt_N100_seed0.npz"
+    np.savez_compressed(os.path.join(HERE, name),
                         conv=conv, inf=inf, steps=st["steps"].astype(np.int16),
                         corrections=st["corrections"].astype(np.int16), hash=track_hash(tr),
                         counts=np.array(O.count_solutions(tr, conv, inf)))
-    print("PH_CodeOpt counts", O.count_solutions(tr, conv, inf), "stages",
+    print("PH" if explicit_rk else "PH_CodeOpt", "counts", O.count_solutions(tr, conv, inf), "stages",
           int(4 * st["steps"].sum() + st["corrections"].sum()))
 
 
@@ -127,9 +129,9 @@ def main():
     loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", "Triplet_Edgels_000.txt"))
     K = O.read_floats(os.path.join(RANS, "Intrinsic_Matrix.txt"), 9)
     tgt, dif, picked = O.prepare_target_params(0, [100], loc, tan, sp)
-    if only == "phcodeopt":
+    if only in ("phcodeopt", "ph"):
         tgt, dif, _ = O.prepare_target_params(0, [100], loc, tan, sp)
-        ph_codeopt_fixture(ss, sp, U, tgt, dif)
+        ph_codeopt_fixture(ss, sp, U, tgt, dif, explicit_rk=only == "ph")
         return
     if only == "heldout":
         heldout_fixture(ss, sp, U)

@@ -287,3 +287,32 @@ def test_ph_codeopt_matches_golden_N100(problem, samples100, tracker):
     assert (r["stats"]["steps"] == g["steps"]).all()
     assert (r["stats"]["corrections"] == g["corrections"]).all()
     assert (track_hash(r["tracks"]) == g["hash"]).all()
+
+
+def test_ph_matches_oracle_small(problem, oracle, samples100, tracker):
+    """The archived ..._PH semantics (explicit RK helpers, no truncation;
+    hc_trifocal_2op1p_30x30_track_ph) on 2 samples vs the oracle, value for value."""
+    tgt, dif, _ = samples100
+    N = 2
+    r = tracker.track(tgt[:N], dif[:N], truncate=False, explicit_rk=True).host()
+    tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, tgt[:N], dif[:N],
+                                           problem.unified_index, oracle.settings(truncate=False, explicit_rk=True))
+    assert (r["converge"] == conv).all() and (r["infinity"] == inf).all()
+    assert (r["stats"]["steps"] == st["steps"]).all()
+    assert (r["stats"]["corrections"] == st["corrections"]).all()
+    assert same(r["tracks"][:, :30], tr[:, :30]).all()
+
+
+def test_ph_matches_golden_N100(problem, samples100, tracker):
+    """Config 2 through the archived ..._PH semantics: every flag / count / track
+    hash equals the oracle's committed run (tests/golden/gpuhc_ph_N100_seed0.npz)."""
+    import sys
+    sys.path.insert(0, GOLDEN)
+    from make_golden import track_hash
+    g = np.load(os.path.join(GOLDEN, "gpuhc_ph_N100_seed0.npz"))
+    tgt, dif, _ = samples100
+    r = tracker.track(tgt, dif, truncate=False, explicit_rk=True).host()
+    assert (r["converge"] == g["conv"]).all() and (r["infinity"] == g["inf"]).all()
+    assert (r["stats"]["steps"] == g["steps"]).all()
+    assert (r["stats"]["corrections"] == g["corrections"]).all()
+    assert (track_hash(r["tracks"]) == g["hash"]).all()

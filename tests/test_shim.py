@@ -41,6 +41,9 @@ SIGNATURES = {
     "kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_Volta":
         "(magma_queue*, int, int, int, int, magmaFloatComplex**, magmaFloatComplex**, magmaFloatComplex*, "
         "magmaFloatComplex*, magmaFloatComplex*, int*, int*, bool*, bool*, magmaFloatComplex*)",
+    "kernel_GPUHC_trifocal_2op1p_30x30_PH":
+        "(magma_queue*, int, int, int, int, magmaFloatComplex**, magmaFloatComplex**, magmaFloatComplex*, "
+        "magmaFloatComplex*, magmaFloatComplex*, int*, int*, bool*, bool*, magmaFloatComplex*)",
 }
 
 
@@ -60,7 +63,7 @@ def _lib():
     L.shim_queue_create.argtypes = [C.c_void_p]
     L.shim_queue_destroy.argtypes = [C.c_void_p]
     for f in ("shim_trunpaths", "shim_trunpaths_volta", "shim_trunransac", "shim_trunransac_volta",
-              "shim_ph_codeopt", "shim_ph_codeopt_volta"):
+              "shim_ph_codeopt", "shim_ph_codeopt_volta", "shim_ph"):
         getattr(L, f).restype = C.c_double
     return L
 
@@ -130,3 +133,37 @@ def test_shim_launchers_match_abi(problem, samples100, tracker, ransac0, abort, 
                         axis=(1, 2))
         assert np.array_equal(got_tr[moved, :30], full["tracks"][moved, :30], equal_nan=True)
         assert (got_conv[moved] == full["converge"][moved]).all()
+
+
+@pytest.mark.gpu
+def test_shim_ph_launcher_matches_abi(problem, samples100, tracker):
+    """The archived ..._PH launcher (separate dH/dx, dH/dt tables) against
+    hc_trifocal_2op1p_30x30_track_ph."""
+    import torch
+    L = _lib()
+    dev = tracker.device
+    N = 2
+    tgt, dif, _ = samples100
+    ref = tracker.track(tgt[:N], dif[:N], truncate=False, explicit_rk=True).host()
+    ss = torch.from_numpy(problem.start_sols).to(dev)
+    tracks = ss.unsqueeze(0).expand(N, -1, -1, -1).reshape(N * 312, 31, 2).contiguous()
+    ssa = torch.tensor([ss.data_ptr() + k * 31 * 8 for k in range(312)], dtype=torch.int64, device=dev)
+    tra = torch.tensor([tracks.data_ptr() + b * 31 * 8 for b in range(312 * N)], dtype=torch.int64, device=dev)
+    sp = torch.from_numpy(problem.start_params).to(dev)
+    tp = torch.from_numpy(np.ascontiguousarray(tgt[:N])).to(dev)
+    dp = torch.from_numpy(np.ascontiguousarray(dif[:N])).to(dev)
+    hx = torch.from_numpy(np.ascontiguousarray(problem.dHdx_index.reshape(-1))).to(dev)
+    ht = torch.from_numpy(np.ascontiguousarray(problem.dHdt_index.reshape(-1))).to(dev)
+    conv = torch.zeros(312 * N, dtype=torch.bool, device=dev)
+    inf = torch.zeros(312 * N, dtype=torch.bool, device=dev)
+    q = L.shim_queue_create(C.c_void_p(torch.cuda.current_stream(dev).cuda_stream))
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    s = tracker.settings
+    rv = L.shim_ph(C.c_void_p(q), C.c_int(N), C.c_int(s.max_steps), C.c_int(s.max_corrections),
+                   C.c_int(s.delta_t_inc_steps), p(ssa), p(tra), p(sp), p(tp), p(dp), p(hx), p(ht), p(conv), p(inf))
+    torch.cuda.synchronize(dev)
+    L.shim_queue_destroy(C.c_void_p(q))
+    assert rv == 0.0
+    assert (conv.cpu().numpy().astype(np.uint8) == ref["converge"]).all()
+    assert (inf.cpu().numpy().astype(np.uint8) == ref["infinity"]).all()
+    assert np.array_equal(tracks.cpu().numpy()[:, :30], ref["tracks"][:, :30], equal_nan=True)

@@ -85,12 +85,13 @@ def lib() -> C.CDLL:
         L.hc_trifocal_version.restype = C.c_char_p
         L.hc_last_error_string.restype = C.c_char_p
         for fn in ("hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
-                   "hc_trifocal_2op1p_30x30_track_ph_codeopt",
+                   "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
                    "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched"):
             getattr(L, fn).restype = C.c_int
         L.hc_trifocal_2op1p_30x30_track.argtypes = [C.POINTER(hcTrackArgs), C.c_void_p, C.c_size_t, C.c_void_p]
         L.hc_trifocal_2op1p_30x30_track_ph_codeopt.argtypes = [C.POINTER(hcTrackArgs), C.c_void_p, C.c_size_t,
                                                                C.c_void_p]
+        L.hc_trifocal_2op1p_30x30_track_ph.argtypes = [C.POINTER(hcTrackArgs), C.c_void_p, C.c_size_t, C.c_void_p]
         L.hc_trifocal_2op1p_30x30_track_abort.argtypes = [C.POINTER(hcTrackArgs), C.POINTER(hcAbortArgs),
                                                           C.c_void_p, C.c_size_t, C.c_void_p]
         L.hc_trifocal_read_timings.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
@@ -133,7 +134,7 @@ def check(status: int, what: str) -> None:
 # Exported symbols that include/*.h declare (tests check the library exports all of them).
 DECLARED_SYMBOLS = (
     "hc_trifocal_workspace_size", "hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
-    "hc_trifocal_2op1p_30x30_track_ph_codeopt",
+    "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
     "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
     "hc_last_error_string",
     "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",

@@ -74,6 +74,7 @@ struct KArgs {
     int num_paths;
     int ordered;        // dequeue track-major in c_track_order (abort mode off)
     int truncate;       // depth-sign path truncation (..._TrunPaths.cu:148-155); 0 = PH_CodeOpt
+    int explicit_rk;    // archived ..._PH: explicit RK helpers (dev-get-new-data.cuh:37-71)
     int max_steps, max_corr, inc_steps;
     const cf *start_sols;
     const cf *const *start_sols_array;
@@ -518,7 +519,15 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         if (act) {
             bool step_end = false;
             if (pred) {
-                if (s < 3) {                                                 // :191-205
+                if (s < 3 && a.explicit_rk) {
+                    // archived ..._PH.cu with dev-get-new-data.cuh:37-71, gc = MAGMA_C_ONE:
+                    // s += ((k*dt)*gc*1.0)/(6|3); x = (s ? x_last : x) + k*((h2|dt)*gc)
+                    const cf kd = cmul(cscale(k, dt), cmk(1.0f, 0.0f));
+                    sols = cadd(sols, cdivs(cscale(kd, 1.0f), s == 0 ? 6.0f : 3.0f));
+                    if (s > 0) x = xl;
+                    x = cadd(x, cmul(k, cmk(s == 2 ? dt : h2, 0.0f)));
+                    if (s != 1) t0 += h2;
+                } else if (s < 3) {                                          // :191-205
                     const float w = (float)((double)coef * 1.0 / 6.0);
                     sols = cadd(sols, cscale(cscale(k, dt), w));
                     if (coef > 1) x = xl;
@@ -704,7 +713,7 @@ static int grid_for(int waves_needed, const void *kernel) {
 }
 
 static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *workspace, size_t wsb,
-                             hcStream stream, bool abort_mode, bool truncate = true) {
+                             hcStream stream, bool abort_mode, bool truncate = true, bool explicit_rk = false) {
     if (!t || t->sub_ransac_iters < 0) return HC_ERROR_INVALID_VALUE;
     if (!workspace || wsb < ws_bytes_needed()) return HC_ERROR_WORKSPACE;
     if (t->sub_ransac_iters == 0) return HC_SUCCESS;
@@ -730,6 +739,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     // abort mode dequeues sample-major, so whole hypotheses finish as early as possible
     k.ordered = abort_mode ? 0 : 1;
     k.truncate = truncate ? 1 : 0;
+    k.explicit_rk = explicit_rk ? 1 : 0;
 #ifdef HC_AB_NATURAL_ORDER
     k.ordered = 0;
 #endif
@@ -821,6 +831,11 @@ hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAb
 hcStatus hc_trifocal_2op1p_30x30_track_ph_codeopt(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,
                                                   hcStream stream) {
     return hc::launch_track(args, nullptr, workspace, workspace_bytes, stream, false, false);
+}
+
+hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,
+                                          hcStream stream) {
+    return hc::launch_track(args, nullptr, workspace, workspace_bytes, stream, false, false, true);
 }
 
 hcStatus hc_trifocal_workspace_status(const void *workspace) {

@@ -102,7 +102,7 @@ class DeviceTracker:
     def launch(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, abort: bool = False,
                stream: torch.cuda.Stream | None = None, workspace: torch.Tensor | None = None,
                sample_offset: int = 0, num_samples: int | None = None, inflight_stop: bool = False,
-               truncate: bool = True) -> None:
+               truncate: bool = True, explicit_rk: bool = False) -> None:
         """Enqueue one tracking run on `stream` (no synchronisation).
 
         Samples [sample_offset, sample_offset + num_samples) of `target`/`diff`
@@ -111,7 +111,8 @@ class DeviceTracker:
         inflight_stop (abort mode): paths in flight also stop once a pose is
         found (hcAbortArgs::inflight_stop; default: the reference's semantics,
         they run to completion).  truncate=False: no depth-sign path
-        truncation (the archived ..._PH_CodeOpt kernel, hc_trifocal_2op1p_30x30_track_ph_codeopt)."""
+        truncation (the archived ..._PH_CodeOpt kernel, hc_trifocal_2op1p_30x30_track_ph_codeopt);
+        with explicit_rk=True as well, the archived ..._PH kernel (hc_trifocal_2op1p_30x30_track_ph)."""
         if num_samples is None:
             num_samples = target.shape[0] - sample_offset
         if num_samples < 0 or sample_offset < 0 or sample_offset + num_samples > target.shape[0] or \
@@ -140,6 +141,8 @@ class DeviceTracker:
         ws = C.c_void_p(ws_t.data_ptr())
         if abort and not truncate:
             raise _abi.HCError("abort mode always truncates paths (..._TrunRANSAC.cu)")
+        if explicit_rk and truncate:
+            raise _abi.HCError("the archived ..._PH kernel has no path truncation: pass truncate=False")
         if abort:
             if self.edgels is None:
                 raise _abi.HCError("abort mode needs set_ransac_data() first")
@@ -152,6 +155,9 @@ class DeviceTracker:
             ab.inflight_stop = 1 if inflight_stop else 0
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track_abort")
+        elif explicit_rk:
+            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph(C.byref(a), ws, self.ws_bytes, hs),
+                       "hc_trifocal_2op1p_30x30_track_ph")
         elif not truncate:
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph_codeopt(C.byref(a), ws, self.ws_bytes, hs),
                        "hc_trifocal_2op1p_30x30_track_ph_codeopt")
@@ -195,13 +201,13 @@ class DeviceTracker:
         return a.value, b.value, hz.value
 
     def track(self, target: np.ndarray, diff: np.ndarray, abort: bool = False, stats: bool = True,
-              inflight_stop: bool = False, truncate: bool = True) -> TrackResult:
+              inflight_stop: bool = False, truncate: bool = True, explicit_rk: bool = False) -> TrackResult:
         """Synchronous convenience wrapper: H2D params, reset tracks, launch, sync, status check."""
         tgt = torch.from_numpy(np.ascontiguousarray(target, np.float32)).to(self.device)
         dif = torch.from_numpy(np.ascontiguousarray(diff, np.float32)).to(self.device)
         r = self.allocate(tgt.shape[0], stats=stats, abort=abort)
         self.reset_tracks(r)
-        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop, truncate=truncate)
+        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop, truncate=truncate, explicit_rk=explicit_rk)
         torch.cuda.synchronize(self.device)
         self.workspace_status()
         return r
