@@ -459,6 +459,32 @@ def cpu_info():
     return model, os.cpu_count(), len(phys) or None
 
 
+def reference_build_cpuhc(threads, n):
+    """The CPU-HC restatement built the way the reference's CPU build is (plain host
+    operators, GCC contraction) and solving through OpenBLAS 0.3.23 `cgesv` with its
+    Haswell kernels -- the configuration that reproduces CPU_Sols_Statistics.txt
+    exactly (tests/test_oracle_kat.py) -- timed on `threads` threads over config-2
+    samples 0..n-1.  Runs tests/cpuhc_pin.py's child in its own process (the
+    OpenBLAS kernel set is chosen when the library loads); None if the image lacks
+    that OpenBLAS."""
+    import subprocess
+    env = dict(os.environ, OPENBLAS_NUM_THREADS="1", OPENBLAS_CORETYPE="Haswell", OMP_NUM_THREADS=str(threads))
+    try:
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "plain"], check=True, capture_output=True)
+        p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "cpuhc_pin.py"), "--child", "plain",
+                            "openblas:Haswell", str(n)], env=env, capture_output=True, text=True, timeout=300)
+        r = json.loads(p.stdout.strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError):
+        return None
+    if "counts" not in r:
+        return None
+    return {"value": round(312 * n / r["seconds"], 1), "cores": threads, "samples": n, "seconds": r["seconds"],
+            "openblas": r.get("openblas_config"),
+            "note": "CPU-HC as the reference builds it: plain MAGMA-order operators with GCC FMA contraction "
+                    "(CMakeLists.txt:36,57) + OpenBLAS 0.3.23 cgesv (Haswell kernels), the configuration that "
+                    "reproduces Output_Write_Files/CPU_Sols_Statistics.txt exactly"}
+
+
 def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
     """CPU baselines on this host's cores, bounded samples of the config-2 workload:
       value        the oracle's CPU-HC restatement (CPUHC_Generic_Solver_Eval_by_Indx
@@ -482,6 +508,7 @@ def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
         return 312 * n / secs, secs
     v, secs = run(n_samples, threads)
     v4, secs4 = run(n_samples_4t, 4)
+    ref = reference_build_cpuhc(threads, n_samples_4t)
     t0 = time.perf_counter()
     O.gpuhc_track(problem.start_sols, problem.start_params, tgt[:n_samples], dif[:n_samples], problem.unified_index,
                   O.settings(threads=threads))
@@ -500,7 +527,9 @@ def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
                                      "seconds": round(secs_p, 2),
                                      "note": "oracle orc_gpuhc_track: the GPU kernel's semantics (depth-sign "
                                              "pruning) on the same threads"},
+            "reference_build": ref,
             "gpu_over_cpu": round(gpu_value / v, 1),
+            "gpu_over_cpu_reference_build": round(gpu_value / ref["value"], 1) if ref and ref.get("value") else None,
             "gpu_over_cpu_pruned": round(gpu_value / vp, 1),
             "gpu_over_cpu_4threads": round(gpu_value / v4, 1)}
 

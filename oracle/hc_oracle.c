@@ -37,9 +37,10 @@ static inline cf cdivs(cf a, float s) { return cmk(a.x / s, a.y / s); }
 #ifdef ORC_PLAIN_OPS
 /* Experiment build only (libhc_oracle_plain.so, tests/cpuhc_pin.py): the
    reference's host operators as plain expressions (MAGMA magma_operators.h
-   order), compiled like the reference CPU build (g++ -O3 -march=native, GCC's
-   default -ffp-contract=fast, CMakeLists.txt:36,57), so the compiler chooses
-   the FMAs as it did for CPU_HC_Solver. */
+   order), compiled like the reference CPU build (-O3 with GCC's default
+   -ffp-contract=fast, CMakeLists.txt:36,57; -march=x86-64-v3 for the reference's
+   -march=native: FMA available), so the compiler chooses the FMAs as it did
+   for CPU_HC_Solver. */
 static inline cf cmul(cf a, cf b) { return cmk(a.x * b.x - a.y * b.y, a.y * b.x + a.x * b.y); }
 static inline cf cmadd(cf acc, cf a, cf b) { return cadd(acc, cmul(a, b)); }
 static inline cf cmsub(cf acc, cf a, cf b) { return csub(acc, cmul(a, b)); }

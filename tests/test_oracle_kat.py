@@ -156,7 +156,7 @@ def test_kat4_cpuhc_counts_exact_with_reference_build_and_openblas():
     """The CPU-HC restatement reproduces the reference's committed counts
     EXACTLY: config 2 (srand(0), 100 samples) gives 11098 / 521 / 6577 when the
     host operators are plain expressions compiled like CMakeLists.txt:36,57
-    (-O3 -march=native, GCC's default -ffp-contract=fast) and every solve goes
+    (-O3, GCC's default -ffp-contract=fast, an FMA-capable -march) and every solve goes
     through OpenBLAS 0.3.23 `cgesv` (CPUHC_Generic_Solver_Eval_by_Indx.cpp:93)
     with its Haswell kernels.  profiles/r2_cpuhc_pin.json has the sweep (spec
     vs plain operators x restated LU vs OpenBLAS Haswell / SkylakeX / Zen /
