@@ -47,7 +47,7 @@ LU_UPDATE_EXECUTED_FRACTION = 0.5859
 LU_EXEC_SAVING = LU_UPDATE_DENSE_FLOP * (1.0 - LU_UPDATE_EXECUTED_FRACTION)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak (64 FLOP/clk/SIMD) == FP32 MFMA peak
 HBM_PEAK_GBS = 8000.0
-TRACK_KERNEL = "void hc::k_track<false, 5, true>(hc::KArgs)"
+TRACK_KERNEL = "void hc::k_track<false, 5, true, false>(hc::KArgs)"
 
 
 def parse():

@@ -11,9 +11,11 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
 base = os.path.join(ROOT, "gpurun_out")
-KPFX = "void hc::k_track"
+# the headline tracker instantiation (archived ablation and abort-mode launches
+# are other instantiations of k_track and are not mixed in)
+KNAME = os.environ.get("HC_PMC_KERNEL", "void hc::k_track<false, 5, true, false>(hc::KArgs)")
 stats = list(csv.DictReader(open(os.path.join(base, f"{tag}_trace", "run_kernel_stats.csv"))))
-trk = [r for r in stats if r["Name"].startswith(KPFX)][0]
+trk = [r for r in stats if r["Name"] == KNAME][0]
 out = {"tag": tag, "version": sys.argv[3] if len(sys.argv) > 3 else None, "kernel": trk["Name"], "calls": int(trk["Calls"]), "avg_ns": float(trk["AverageNs"]),
        "min_ns": float(trk["MinNs"]), "max_ns": float(trk["MaxNs"]), "counters": {}}
 meta = None
@@ -24,7 +26,7 @@ for d in sorted(glob.glob(os.path.join(base, f"{tag}_pmc*"))):
     agg = collections.defaultdict(float)
     disp = set()
     for r in csv.DictReader(open(f)):
-        if r["Kernel_Name"].startswith(KPFX):
+        if r["Kernel_Name"] == KNAME:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
             disp.add(r["Dispatch_Id"])
             meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "Scratch_Size", "VGPR_Count",

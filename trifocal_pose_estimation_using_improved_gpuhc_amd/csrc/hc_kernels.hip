@@ -240,7 +240,10 @@ __device__ unsigned long long g_diag_phase[13];
 // MINW: waves per SIMD the register allocation targets.  GTAB: the term tables
 // are read from the workspace (global, L1/L2-resident) instead of being staged
 // in LDS, which leaves 27.6 KB LDS per workgroup (5 workgroups per CU).
-template <bool ABORT, int MINW, bool GTAB>
+// ARCH: the archived ablation semantics (KArgs::truncate / explicit_rk read at
+// run time); a separate instantiation so the headline kernel carries neither
+// switch and the two show up under their own names in a kernel trace.
+template <bool ABORT, int MINW, bool GTAB, bool ARCH = false>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     constexpr int TAB_BYTES = GTAB ? 16 : (int)(sizeof(uint2) * (HX_SLOT_CAP + HT_TERMS) * 32);
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
@@ -381,7 +384,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         sols = rl ? dstart[r] : cmk(0.0f, 0.0f);
                         xl = x;
                         t0 = 0.0f; t_step = 0.0f; dt = 0.01f;                 // :80
-                        end_zone = false; check = a.truncate != 0; isSucc = false; isInf = false;
+                        end_zone = false; check = !ARCH || a.truncate != 0; isSucc = false; isInf = false;
                         succ = 0; nsteps = 0; ncorr = 0; stepidx = 0;
                         ph = PH_BEGIN;
                     }
@@ -519,7 +522,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         if (act) {
             bool step_end = false;
             if (pred) {
-                if (s < 3 && a.explicit_rk) {
+                if (ARCH && s < 3 && a.explicit_rk) {
                     // archived ..._PH.cu with dev-get-new-data.cuh:37-71, gc = MAGMA_C_ONE:
                     // s += ((k*dt)*gc*1.0)/(6|3); x = (s ? x_last : x) + k*((h2|dt)*gc)
                     const cf kd = cmul(cscale(k, dt), cmk(1.0f, 0.0f));
@@ -760,7 +763,11 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     // tracking: term tables read from the workspace (L1/L2), 96 VGPRs, 27.6 KB LDS
     // per workgroup -> 5 waves/SIMD.  Abort mode keeps the tables in LDS at 4
     // waves/SIMD (the scoring path needs the registers).
-    const void *kern = abort_mode ? (const void *)k_track<true, 4, false> : (const void *)k_track<false, 5, true>;
+    const bool archived = !truncate || explicit_rk;
+    if (abort_mode && archived) return HC_ERROR_INVALID_VALUE;
+    const void *kern = abort_mode ? (const void *)k_track<true, 4, false>
+                       : archived ? (const void *)k_track<false, 5, true, true>
+                                  : (const void *)k_track<false, 5, true>;
     const int grid = grid_for((int)((paths + 1) / 2), kern);
     if (grid <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
