@@ -116,7 +116,7 @@ def main():
     NP = max(NS, args.pipelined_streams)
     streams = [stream] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
     bufs = [res] + [tr.allocate(S, stats=True) for _ in range(NP - 1)]
-    wss = [tr.workspace] + [tr.new_workspace() for _ in range(NP - 1)]
+    wss = [tr.new_workspace(S) for _ in range(NP)]
 
     def step(i, ns):
         k = i % ns

@@ -38,17 +38,29 @@ constexpr int kHxInts = 36000, kHtInts = 2880;   // dHdx_Index_Matrix_Size, dHdt
 
 struct StreamState {
     void *workspace = nullptr;
+    size_t ws_bytes = 0;
     int32_t *unified = nullptr;   // Volta variants only
 };
 
-StreamState *state_for(hipStream_t s, bool need_unified) {
+// the stream's workspace, grown to time-slicing size for launches of N samples
+// (hc_trifocal_workspace_size_for; N = 0: abort mode, the base size)
+StreamState *state_for(hipStream_t s, bool need_unified, int N = 0) {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, StreamState> states;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(mu);
     StreamState &st = states[{dev, s}];
-    if (!st.workspace && hipMalloc(&st.workspace, hc_trifocal_workspace_size()) != hipSuccess) st.workspace = nullptr;
+    const size_t need = N > 0 ? hc_trifocal_workspace_size_for(N) : hc_trifocal_workspace_size();
+    if (st.workspace && st.ws_bytes < need) {
+        // the previous launch on this stream may still use it
+        if (hipStreamSynchronize(s) != hipSuccess || hipFree(st.workspace) != hipSuccess) return nullptr;
+        st.workspace = nullptr;
+    }
+    if (!st.workspace) {
+        if (hipMalloc(&st.workspace, need) != hipSuccess) st.workspace = nullptr;
+        st.ws_bytes = st.workspace ? need : 0;
+    }
     if (need_unified && !st.unified &&
         hipMalloc(reinterpret_cast<void **>(&st.unified), (kHxInts + kHtInts) * sizeof(int32_t)) != hipSuccess)
         st.unified = nullptr;
@@ -93,12 +105,12 @@ real_Double_t track(magma_queue_t q, int N, int max_steps, int max_corr, int inc
                     const int *unified, const int *d_hx, const int *d_ht, bool *conv, bool *inf, const char *name,
                     bool truncate = true, bool explicit_rk = false) {
     hipStream_t s = magma_queue_get_hip_stream(q);
-    StreamState *st = state_for(s, unified == nullptr);
+    StreamState *st = state_for(s, unified == nullptr, N);
     if (!st) { report(HC_ERROR_WORKSPACE, name); return 0.0; }
     const int32_t *U = unified ? reinterpret_cast<const int32_t *>(unified) : unify(st, d_hx, d_ht, s);
     if (!U) { report(HC_ERROR_LAUNCH, name); return 0.0; }
     hcTrackArgs a = make_args(N, max_steps, max_corr, inc_steps, ss, tracks, sp, tp, dp, U, conv, inf);
-    const size_t wsb = hc_trifocal_workspace_size();
+    const size_t wsb = st->ws_bytes;
     report(explicit_rk ? hc_trifocal_2op1p_30x30_track_ph(&a, st->workspace, wsb, (hcStream)s)
            : truncate  ? hc_trifocal_2op1p_30x30_track(&a, st->workspace, wsb, (hcStream)s)
                        : hc_trifocal_2op1p_30x30_track_ph_codeopt(&a, st->workspace, wsb, (hcStream)s),

@@ -158,6 +158,25 @@ def test_tracker_matches_golden_N100(problem, samples100, tracker):
     assert tuple(g["counts"]) == count_solutions(r["tracks"], r["converge"], r["infinity"])
 
 
+def test_time_slicing_is_bit_exact(problem, samples100, tracker):
+    """Time slicing (paths suspended at step boundaries and resumed by any slot,
+    hc_trifocal_workspace_size_for) changes when a path runs, never what it
+    computes: the config-2 run with and without it agree bit for bit (sign of
+    zero and NaN payloads included), and the sliced run did suspend paths."""
+    tgt, dif, _ = samples100
+    a = tracker.track(tgt, dif, time_slicing=False).host()
+    b = tracker.track(tgt, dif, time_slicing=True).host()
+    # ring counters after the base workspace (hc_kernels.hip KArgs::rq): [0] head, [64] tail, [128] avail
+    off = int(tracker.L.hc_trifocal_workspace_size())
+    rq = np.frombuffer(tracker.workspace[off:off + 768].cpu().numpy().tobytes(), np.uint32)
+    assert rq[64] > 1000, f"only {rq[64]} suspensions"
+    assert rq[0] == rq[64] and rq[128] == 0, "every suspended path was resumed"
+    assert (a["converge"] == b["converge"]).all() and (a["infinity"] == b["infinity"]).all()
+    assert np.array_equal(a["stats"]["steps"], b["stats"]["steps"])
+    assert np.array_equal(a["stats"]["corrections"], b["stats"]["corrections"])
+    assert np.array_equal(a["tracks"].view(np.uint32), b["tracks"].view(np.uint32))
+
+
 def test_tracker_abort_mode(problem, samples100, tracker):
     """Config 3 semantics (abort on): the found hypothesis is one of the passing
     hypotheses of the abort-off run; tracked paths equal the abort-off results;

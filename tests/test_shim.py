@@ -69,15 +69,15 @@ def _lib():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("abort,truncate", [(False, True), (True, True), (False, False)])
-@pytest.mark.parametrize("volta", [False, True])
-def test_shim_launchers_match_abi(problem, samples100, tracker, ransac0, abort, truncate, volta):
+@pytest.mark.parametrize("abort,truncate,volta,N", [
+    (a, t, v, 3) for (a, t) in [(False, True), (True, True), (False, False)] for v in (False, True)] + [
+    (False, True, False, 100)])   # enough paths for time slicing: suspended x goes through the pointer arrays
+def test_shim_launchers_match_abi(problem, samples100, tracker, ransac0, abort, truncate, volta, N):
     """truncate=False: the archived ..._PH_CodeOpt[_Volta] launchers against
     hc_trifocal_2op1p_30x30_track_ph_codeopt."""
     import torch
     L = _lib()
     dev = tracker.device
-    N = 3
     tgt, dif, _ = samples100
     ref = tracker.track(tgt[:N], dif[:N], abort=abort, truncate=truncate).host()
     # the reference's device layout (GPU_HC_Solver.cpp:137-184,335-362): start sols and

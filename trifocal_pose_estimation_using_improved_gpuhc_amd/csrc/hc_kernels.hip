@@ -44,7 +44,15 @@ __constant__ int c_track_order[NTRK] = {
 #include "hc_track_order.inc"
 #endif
 };
+#ifdef HC_AB_PATH_ORDER
+// experiment build only: an explicit per-path dequeue order (device array set
+// by hc_ab_set_path_order), to bound what any dequeue order can gain
+__device__ const int *g_ab_path_order = nullptr;
+#endif
 __device__ __forceinline__ int path_of_queue_pos(int q, int num_paths, int ordered) {
+#ifdef HC_AB_PATH_ORDER
+    if (g_ab_path_order) return g_ab_path_order[q];
+#endif
     if (!ordered) return q;
     const int n = num_paths / NTRK;          // samples in this launch
     const int rank = q / n;
@@ -70,6 +78,35 @@ struct Workspace {
 };
 static_assert(offsetof(Workspace, tab) == 64, "control block is 64 bytes");
 
+// Time slicing.  A path that has run slice_q steps while other
+// work waits is suspended at its step boundary: x goes to its own track entry,
+// the step-control scalars to PathState, the path id to a FIFO ring.  While
+// new paths remain, the suspending half takes one (an unpaired push); after
+// that it swaps with the oldest suspended path (a paired push + pop, i.e.
+// round robin).  A half whose path ends takes a new path, else the oldest
+// suspended one.  Every path thus starts early and the end of a launch is
+// made of short remainders instead of whole late-dequeued long paths.
+// Bit-exact: at a step boundary x == x_last == the RK accumulator, and this
+// is the whole vector state.
+//
+// Ring protocol (no CAS loops): tickets from atomicAdd on head / tail; avail
+// counts published entries not yet claimed by unpaired pops (a semaphore:
+// decrement, undo if it was empty and retry while the undo leaves it
+// positive, so concurrent failures cannot hide an entry).  A paired pop needs
+// no claim: its own push precedes it.  A claimed entry may still be in the
+// pusher's hands (ticket taken, entry not yet written), hence the short wait
+// on its sequence tag.
+struct PathState {
+    float t0, dt;
+    int stepidx, nsteps, ncorr, succ, flags, pad;
+};
+static_assert(sizeof(PathState) == 32, "PathState is 32 bytes");
+#ifndef HC_SLICE_Q
+#define HC_SLICE_Q 3
+#endif
+constexpr int SLICE_Q = HC_SLICE_Q;          // steps per time slice (0: no slicing)
+constexpr unsigned RING_SLACK = 1u << 16;    // ring entries beyond one per path (> 2x the path slots)
+
 struct KArgs {
     int num_paths;
     int ordered;        // dequeue track-major in c_track_order (abort mode off)
@@ -94,7 +131,74 @@ struct KArgs {
     const float *K;
     uint8_t *found_flag;
     int32_t *batch_index;
+    // time slicing (slice_q > 0; tracking without abort only)
+    int slice_q;
+    unsigned ring_cap;
+    unsigned *rq;                   // ring counters, one 256-B line each: [0] head, [64] tail, [128] avail
+    PathState *pst;                 // per path id
+    unsigned long long *ring;       // (ticket + 1) << 32 | path id
 };
+constexpr int RQ_HEAD = 0, RQ_TAIL = 64, RQ_AVAIL = 128, RQ_WORDS = 192;
+
+__device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the hand-over data of a suspended path is written and read with agent-scope
+// relaxed atomics (coherent across the XCDs' L2s without cache-wide fences);
+// the writer drains its stores (s_waitcnt vmcnt(0)) before publishing the ring
+// entry, and the reader's loads depend on the entry's path id
+__device__ __forceinline__ void st_cf_rlx(cf *p, cf v) {
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
+                       (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ cf ld_cf_rlx(const cf *p) {
+    const unsigned long long u =
+        __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return cmk(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
+}
+__device__ __forceinline__ void st_i_rlx(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ld_i_rlx(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
+
+// (pointers and sizes by value: a KArgs reference would put the kernel
+// arguments in scratch memory)
+__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, int b, bool unpaired) {
+    const unsigned t = atomicAdd(&rq[RQ_TAIL], 1u);
+    __hip_atomic_store(&ring[t % cap], ((unsigned long long)(t + 1u) << 32) | (unsigned)b, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (unpaired) {
+        drain_stores();
+        atomicAdd(&rq[RQ_AVAIL], 1u);
+    }
+}
+// the entry of claimed ticket h (bounded wait; HC_ERROR_DEVICE in the status if it never comes)
+__device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigned cap, Workspace *ws, unsigned h) {
+    for (int spin = 0; spin < (1 << 22); spin++) {
+        const unsigned long long e = __hip_atomic_load(&ring[h % cap], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((unsigned)(e >> 32) == h + 1u) return (int)(unsigned)e;
+        __builtin_amdgcn_s_sleep(2);
+    }
+    atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
+    return -1;
+}
+__device__ __forceinline__ int ring_pop_paired(unsigned *rq, const unsigned long long *ring, unsigned cap,
+                                               Workspace *ws) {
+    return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u));
+}
+// oldest suspended path id, or -1 if there is none
+__device__ __forceinline__ int ring_pop(unsigned *rq, const unsigned long long *ring, unsigned cap, Workspace *ws) {
+    int *avail = reinterpret_cast<int *>(&rq[RQ_AVAIL]);
+    if (ld_i_rlx(avail) <= 0) return -1;
+    for (;;) {
+        if (atomicSub(avail, 1) > 0) return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u));
+        if (atomicAdd(avail, 1) + 1 <= 0) return -1;
+    }
+}
 
 // ---------------------------------------------------------------- table prep
 // Compacts the reference's padded unified index (38880 ints: dH/dx at
@@ -294,6 +398,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     int diag_t0 = 0;
 #endif
     int s = 0, stepidx = 0, coef = 1, succ = 0, nsteps = 0, ncorr = 0;
+    int piece = 0;   // steps since the path (re)started on this slot (time slicing)
     float t0 = 0.0f, t_step = 0.0f, dt = 0.01f, h2 = 0.0f, scale = 0.0f;
     bool end_zone = false, check = true, isSucc = false, isInf = false;
     cf x = cmk(0.0f, 0.0f), xl = x, sols = x;
@@ -308,6 +413,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     for (;;) {
         HC_DIAG_MARK(6);
         // ---------------- resolve slot phases until every slot is at a stage or idle
+        // next dequeue (time slicing): -1 normal, -2 swap with a suspended path,
+        // >= 0 a new-path ticket the suspension claimed (set and used within this phase)
+        int deq_hint = -1;
         for (;;) {
             if (ph == PH_FINISH) {                                            // :282-286
                 const bool conv = ((double)t0 >= 1.0 || (1.0 - (double)t0 <= 0.0000001));
@@ -344,10 +452,54 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                 ph = PH_DEQ;
             }
             if (ph == PH_DEQ) {
-                int nb = 0;
-                if (r == 0) nb = (int)atomicAdd(&ws->queue, 1u);
+                int nb = 0, rb = -1;   // new-path ticket; else a suspended path id (time slicing)
+                if (r == 0) {
+                    if (!ABORT && deq_hint >= 0) {
+                        nb = deq_hint;                       // claimed by the suspension
+                    } else if (!ABORT && deq_hint == -2) {
+                        nb = a.num_paths;                    // swap: the oldest suspended path
+                        rb = ring_pop_paired(a.rq, a.ring, a.ring_cap, ws);
+                    } else {
+                        nb = (ABORT || a.slice_q == 0 || ld_rlx(&ws->queue) < (unsigned)a.num_paths)
+                                 ? (int)atomicAdd(&ws->queue, 1u) : a.num_paths;
+                        if (!ABORT && nb >= a.num_paths && a.slice_q > 0) rb = ring_pop(a.rq, a.ring, a.ring_cap, ws);
+                    }
+                }
+                deq_hint = -1;
                 nb = bperm_i(nb, hb);
-                if (nb >= a.num_paths) {
+                if (!ABORT) rb = bperm_i(rb, hb);
+                if (!ABORT && rb >= 0) {
+                    // resume a suspended path at its step boundary (the state the
+                    // suspending slot stored: x in the path's own track entry)
+                    b = rb;
+                    qpos = 0;
+                    const int smp = b / NTRK;
+                    if (smp != smp_loaded && r < NPP) {
+                        S.tgt[r] = a.target_params[(size_t)smp * NPP + r];
+                        S.dif[r] = a.diff_params[(size_t)smp * NPP + r];
+                    }
+                    if (smp != smp_loaded && r < NPP - 32) {
+                        S.tgt[r + 32] = a.target_params[(size_t)smp * NPP + r + 32];
+                        S.dif[r + 32] = a.diff_params[(size_t)smp * NPP + r + 32];
+                    }
+                    smp_loaded = smp;
+                    const cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+                    x = rl ? ld_cf_rlx(dtrack + r) : cmk(0.0f, 0.0f);
+                    xl = x;
+                    sols = x;
+                    const int *q = reinterpret_cast<const int *>(a.pst + b);
+                    t0 = __int_as_float(ld_i_rlx(q + 0));
+                    dt = __int_as_float(ld_i_rlx(q + 1));
+                    stepidx = ld_i_rlx(q + 2);
+                    nsteps = ld_i_rlx(q + 3);
+                    ncorr = ld_i_rlx(q + 4);
+                    succ = ld_i_rlx(q + 5);
+                    const int fl = ld_i_rlx(q + 6);
+                    end_zone = (fl & 1) != 0; check = (fl & 2) != 0; isSucc = false; isInf = false;
+                    t_step = 0.0f;
+                    piece = 0;
+                    ph = PH_BEGIN;
+                } else if (nb >= a.num_paths) {
                     ph = PH_IDLE;
                     b = -1;
                 } else {
@@ -385,7 +537,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         xl = x;
                         t0 = 0.0f; t_step = 0.0f; dt = 0.01f;                 // :80
                         end_zone = false; check = !ARCH || a.truncate != 0; isSucc = false; isInf = false;
-                        succ = 0; nsteps = 0; ncorr = 0; stepidx = 0;
+                        succ = 0; nsteps = 0; ncorr = 0; stepidx = 0; piece = 0;
                         ph = PH_BEGIN;
                     }
                 }
@@ -414,7 +566,42 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     }
                     done = (double)t0 > 0.95 && check;
                 }
-                if (!done) {
+                bool suspend = false;
+                if (!ABORT && !done && a.slice_q > 0 && piece >= a.slice_q) {
+                    // time slice used up: suspend for a new path (its ticket
+                    // claimed here), else swap with a suspended path, else
+                    // keep running
+                    int hint = -1;
+                    if (r == 0) {
+                        if (ld_rlx(&ws->queue) < (unsigned)a.num_paths) {
+                            const int t = (int)atomicAdd(&ws->queue, 1u);
+                            if (t < a.num_paths) hint = t;
+                        }
+                        if (hint < 0 && ld_i_rlx(reinterpret_cast<const int *>(&a.rq[RQ_AVAIL])) > 0) hint = -2;
+                    }
+                    hint = bperm_i(hint, hb);
+                    if (hint != -1) {
+                        cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
+                        if (rl) st_cf_rlx(dtrack + r, x);
+                        if (r == 0) {
+                            int *q = reinterpret_cast<int *>(a.pst + b);
+                            st_i_rlx(q + 0, __float_as_int(t0));
+                            st_i_rlx(q + 1, __float_as_int(dt));
+                            st_i_rlx(q + 2, stepidx);
+                            st_i_rlx(q + 3, nsteps);
+                            st_i_rlx(q + 4, ncorr);
+                            st_i_rlx(q + 5, succ);
+                            st_i_rlx(q + 6, (end_zone ? 1 : 0) | (check ? 2 : 0));
+                        }
+                        drain_stores();
+                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, b, hint >= 0);
+                        deq_hint = hint;
+                        suspend = true;
+                    } else {
+                        piece = 0;
+                    }
+                }
+                if (!done && !suspend) {
                     if (end_zone) {
                         if (dt > __builtin_fabsf(1.0f - t0)) dt = __builtin_fabsf(1.0f - t0);
                     } else if ((double)dt > __builtin_fabs(0.95 - (double)t0)) {
@@ -426,18 +613,20 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     coef = 1;
                     s = 0;
                     nsteps++;
+                    piece++;
                 }
-                ph = done ? PH_FINISH : PH_STAGE;
+                ph = suspend ? PH_DEQ : done ? PH_FINISH : PH_STAGE;
             }
             if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
         }
         if (__ballot(ph == PH_STAGE) == 0ull) break;
-        if (!ABORT && a.ordered) {
-            // Issue priority by queue position (s_setprio, arbitration among the
-            // waves of a SIMD): the last tenth of the queue at 3, the tenth
-            // before at 2, the one before that at 1.  Paths dequeued late
-            // decide when the launch ends; the earlier ones have slack
-            // (profiles/r2_ab_priority.jsonl: -1.8 %).
+        if (!ABORT && a.ordered && a.slice_q == 0) {
+            // Without time slicing: issue priority by queue position (s_setprio,
+            // arbitration among the waves of a SIMD): the last tenth of the
+            // queue at 3, the tenth before at 2, the one before that at 1.
+            // Paths dequeued late decide when the launch ends; the earlier
+            // ones have slack (profiles/r2_ab_priority.jsonl:
+            // -1.8 %).  With slicing it is neutral (profiles/r2n_ab_slice2.jsonl).
             const int qp = (ph == PH_STAGE) ? qpos : 0;
             const int m = max(__builtin_amdgcn_readlane(qp, 0), __builtin_amdgcn_readlane(qp, 32));
             const int lvl = (int)((long long)m * PRIO_TENTHS / a.num_paths);
@@ -457,8 +646,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             q.t0 = t0; q.t_step = t_step; q.dt = dt; q.h2 = h2; q.scale = scale;
             q.s = s; q.stepidx = stepidx; q.coef = coef; q.succ = succ; q.nsteps = nsteps; q.ncorr = ncorr;
             q.b = b; q.smp = smp_loaded; q.ph = ph;
-            q.flags = (end_zone ? 1 : 0) | (check ? 2 : 0) | (isSucc ? 4 : 0) | (isInf ? 8 : 0);
-            q.pad = 0;
+            q.flags = (end_zone ? 1 : 0) | (check ? 2 : 0) | (isSucc ? 4 : 0) | (isInf ? 8 : 0) | (piece << 4);
+            q.pad = qpos;
             S.st = q;
         }
         if (rl) { S.x[r] = x; S.xl[r] = xl; S.sols[r] = sols; }
@@ -515,6 +704,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             s = q.s; stepidx = q.stepidx; coef = q.coef; succ = q.succ; nsteps = q.nsteps; ncorr = q.ncorr;
             b = q.b; smp_loaded = q.smp; ph = q.ph;
             end_zone = q.flags & 1; check = q.flags & 2; isSucc = q.flags & 4; isInf = q.flags & 8;
+            piece = q.flags >> 4;
+            qpos = q.pad;
             x = rl ? S.x[r] : cmk(0.0f, 0.0f);
             xl = rl ? S.xl[r] : cmk(0.0f, 0.0f);
             sols = rl ? S.sols[r] : cmk(0.0f, 0.0f);
@@ -689,6 +880,12 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
 
 // ---------------------------------------------------------------- host side
 static size_t ws_bytes_needed() { return (sizeof(Workspace) + 255) & ~(size_t)255; }
+// + the time-slicing area of a launch of `paths` paths: PathState per path, then the ring
+static size_t ws_bytes_for(long long paths) {
+    if (paths < 0) paths = 0;
+    return ws_bytes_needed() + ((RQ_WORDS * sizeof(unsigned) + (size_t)paths * sizeof(PathState) +
+                                 ((size_t)paths + RING_SLACK) * sizeof(unsigned long long) + 255) & ~(size_t)255);
+}
 
 // Persistent grid: resident workgroups (occupancy API, cached per device and
 // kernel) x CUs, capped by the work.
@@ -760,6 +957,19 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.inf = t->infinity;
     k.stats = t->stats;
     k.ws = ws;
+    // time slicing when the workspace has room for it (hc_trifocal_workspace_size_for)
+    if (!abort_mode && SLICE_Q > 0 && wsb >= ws_bytes_for(paths)) {
+        char *base = (char *)workspace + ws_bytes_needed();
+        k.rq = (unsigned *)base;
+        k.pst = (PathState *)(base + RQ_WORDS * sizeof(unsigned));
+        k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) + (size_t)paths * sizeof(PathState));
+        k.ring_cap = (unsigned)(paths + RING_SLACK);
+        k.slice_q = SLICE_Q;
+        // counters + ring zeroed (sequence tags of an earlier launch never match)
+        if ((g_last_hip_error = hipMemsetAsync(k.rq, 0, RQ_WORDS * sizeof(unsigned), s)) != hipSuccess ||
+            (g_last_hip_error = hipMemsetAsync(k.ring, 0, sizeof(unsigned long long) * k.ring_cap, s)) != hipSuccess)
+            return HC_ERROR_LAUNCH;
+    }
     // tracking: term tables read from the workspace (L1/L2), 96 VGPRs, 27.6 KB LDS
     // per workgroup -> 5 waves/SIMD.  Abort mode keeps the tables in LDS at 4
     // waves/SIMD (the scoring path needs the registers).
@@ -825,6 +1035,10 @@ int hc_diag_luwork(unsigned long long *out, int reset) {
 
 size_t hc_trifocal_workspace_size(void) { return hc::ws_bytes_needed(); }
 
+size_t hc_trifocal_workspace_size_for(int sub_ransac_iters) {
+    return hc::ws_bytes_for(sub_ransac_iters > 0 ? (long long)sub_ransac_iters * hc::NTRK : 0);
+}
+
 hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,
                                        hcStream stream) {
     return hc::launch_track(args, nullptr, workspace, workspace_bytes, stream, false);
@@ -850,7 +1064,8 @@ hcStatus hc_trifocal_workspace_status(const void *workspace) {
     hc::Workspace h;
     const hcStatus st = hc::read_control(workspace, h);
     if (st != HC_SUCCESS) return st;
-    return h.status ? HC_ERROR_TABLE : HC_SUCCESS;
+    if (h.status == 0u) return HC_SUCCESS;
+    return h.status == (unsigned)HC_ERROR_TABLE ? HC_ERROR_TABLE : HC_ERROR_DEVICE;
 }
 
 hcStatus hc_trifocal_read_timings(const void *workspace, double *first_found_seconds) {
@@ -910,6 +1125,14 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
 }
 
 const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
+
+#ifdef HC_AB_PATH_ORDER
+// experiment build only: dequeue order = order[q] (a device array of the
+// launch's path ids, or null for the built-in order)
+int hc_ab_set_path_order(const int *order) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_ab_path_order), &order, sizeof(order)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 const char *hc_trifocal_version(void) {
     return "hc_trifocal gfx950 v9.1 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "

@@ -102,7 +102,7 @@ class DeviceTracker:
     def launch(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, abort: bool = False,
                stream: torch.cuda.Stream | None = None, workspace: torch.Tensor | None = None,
                sample_offset: int = 0, num_samples: int | None = None, inflight_stop: bool = False,
-               truncate: bool = True, explicit_rk: bool = False) -> None:
+               truncate: bool = True, explicit_rk: bool = False, time_slicing: bool = True) -> None:
         """Enqueue one tracking run on `stream` (no synchronisation).
 
         Samples [sample_offset, sample_offset + num_samples) of `target`/`diff`
@@ -112,16 +112,25 @@ class DeviceTracker:
         found (hcAbortArgs::inflight_stop; default: the reference's semantics,
         they run to completion).  truncate=False: no depth-sign path
         truncation (the archived ..._PH_CodeOpt kernel, hc_trifocal_2op1p_30x30_track_ph_codeopt);
-        with explicit_rk=True as well, the archived ..._PH kernel (hc_trifocal_2op1p_30x30_track_ph)."""
+        with explicit_rk=True as well, the archived ..._PH kernel (hc_trifocal_2op1p_30x30_track_ph).
+        time_slicing (tracking launches): suspend and resume paths at step
+        boundaries so every path starts early (hc_trifocal_workspace_size_for;
+        bit-identical results).  The default workspace grows to the size that
+        enables it; a caller's workspace enables it if it is large enough."""
         if num_samples is None:
             num_samples = target.shape[0] - sample_offset
         if num_samples < 0 or sample_offset < 0 or sample_offset + num_samples > target.shape[0] or \
                 (sample_offset + num_samples) * 312 > r.tracks.shape[0]:
             raise _abi.HCError("sample range outside the buffers")
         p0, p1 = sample_offset * 312, (sample_offset + num_samples) * 312
+        if workspace is None and not abort and time_slicing:
+            need = int(self.L.hc_trifocal_workspace_size_for(num_samples))
+            if self.workspace.numel() < need:
+                self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
         ws_t = workspace if workspace is not None else self.workspace
         if ws_t.numel() < self.ws_bytes:
             raise _abi.HCError("workspace too small")
+        wsb = ws_t.numel() if (time_slicing and not abort) else self.ws_bytes
         a = _abi.hcTrackArgs()
         a.sub_ransac_iters = num_samples
         a.settings = self.settings
@@ -153,20 +162,23 @@ class DeviceTracker:
             ab.found_trifocal_sols = r.found.data_ptr()
             ab.trifocal_sols_batch_index = r.batch_index[p0:p1].data_ptr()
             ab.inflight_stop = 1 if inflight_stop else 0
-            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, self.ws_bytes, hs),
+            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, wsb, hs),
                        "hc_trifocal_2op1p_30x30_track_abort")
         elif explicit_rk:
-            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph(C.byref(a), ws, self.ws_bytes, hs),
+            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph(C.byref(a), ws, wsb, hs),
                        "hc_trifocal_2op1p_30x30_track_ph")
         elif not truncate:
-            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph_codeopt(C.byref(a), ws, self.ws_bytes, hs),
+            _abi.check(self.L.hc_trifocal_2op1p_30x30_track_ph_codeopt(C.byref(a), ws, wsb, hs),
                        "hc_trifocal_2op1p_30x30_track_ph_codeopt")
         else:
-            _abi.check(self.L.hc_trifocal_2op1p_30x30_track(C.byref(a), ws, self.ws_bytes, hs),
+            _abi.check(self.L.hc_trifocal_2op1p_30x30_track(C.byref(a), ws, wsb, hs),
                        "hc_trifocal_2op1p_30x30_track")
 
-    def new_workspace(self) -> torch.Tensor:
-        return torch.zeros(self.ws_bytes, dtype=torch.uint8, device=self.device)
+    def new_workspace(self, num_samples: int = 0) -> torch.Tensor:
+        """A workspace; with num_samples > 0, large enough for time slicing of
+        tracking launches of up to that many samples."""
+        n = int(self.L.hc_trifocal_workspace_size_for(num_samples)) if num_samples > 0 else self.ws_bytes
+        return torch.zeros(n, dtype=torch.uint8, device=self.device)
 
     def launch_abort_chunked(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, chunk_samples: int,
                              workspaces: list, group=None, stream: torch.cuda.Stream | None = None,
@@ -201,13 +213,15 @@ class DeviceTracker:
         return a.value, b.value, hz.value
 
     def track(self, target: np.ndarray, diff: np.ndarray, abort: bool = False, stats: bool = True,
-              inflight_stop: bool = False, truncate: bool = True, explicit_rk: bool = False) -> TrackResult:
+              inflight_stop: bool = False, truncate: bool = True, explicit_rk: bool = False,
+              time_slicing: bool = True) -> TrackResult:
         """Synchronous convenience wrapper: H2D params, reset tracks, launch, sync, status check."""
         tgt = torch.from_numpy(np.ascontiguousarray(target, np.float32)).to(self.device)
         dif = torch.from_numpy(np.ascontiguousarray(diff, np.float32)).to(self.device)
         r = self.allocate(tgt.shape[0], stats=stats, abort=abort)
         self.reset_tracks(r)
-        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop, truncate=truncate, explicit_rk=explicit_rk)
+        self.launch(tgt, dif, r, abort=abort, inflight_stop=inflight_stop, truncate=truncate, explicit_rk=explicit_rk,
+                    time_slicing=time_slicing)
         torch.cuda.synchronize(self.device)
         self.workspace_status()
         return r
