@@ -67,6 +67,19 @@ def test_workspace_size_and_version():
     assert b"gfx950" in L.hc_trifocal_version()
 
 
+def test_workspace_size_for_time_slicing():
+    """hc_trifocal_workspace_size_for(N): the base workspace + the time-slicing
+    area (ring counters, 32-B PathState per path, 8-B ring entry per path + slack)."""
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+    L = _abi.lib()
+    base = int(L.hc_trifocal_workspace_size())
+    s0, s1, s100 = (int(L.hc_trifocal_workspace_size_for(n)) for n in (0, 1, 100))
+    assert base < s0 <= s1 < s100
+    assert s100 % 256 == 0
+    assert 40 * 312 * 100 <= s100 - base <= 40 * 312 * 100 + (1 << 20)
+    assert int(L.hc_trifocal_workspace_size_for(-5)) == s0
+
+
 def test_invalid_arguments_are_rejected_before_any_device_work():
     from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
     L = _abi.lib()
