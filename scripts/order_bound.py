@@ -38,6 +38,8 @@ def main():
     L = _abi.lib()
     L.hc_ab_set_path_order.argtypes = [C.c_void_p]
     L.hc_ab_set_path_order.restype = C.c_int
+    if "--timeline" in sys.argv:
+        L.hc_diag_span.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     tr = DeviceTracker(problem, dev)
     r = tr.allocate(100)
     t, d = torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev)
@@ -57,7 +59,10 @@ def main():
             ot = None if o is None else torch.from_numpy(o.astype(np.int32)).to(dev)
             assert L.hc_ab_set_path_order(None if ot is None else C.c_void_p(ot.data_ptr())) == 0
             ms = []
+            kspan = (C.c_ulonglong * 4)()
             for i in range(8):
+                if "--timeline" in sys.argv:
+                    L.hc_diag_span(kspan, 1)      # reset: the last launch's span is read below
                 tr.reset_tracks(r)
                 a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record(s)
@@ -81,6 +86,11 @@ def main():
                            last_dequeue_ms=round(float(t0.max()), 3),
                            finish_ms_q=[round(float(v), 2) for v in np.percentile(t1, [50, 90, 99, 99.9, 100])],
                            finished_in_last_2ms=int((t1 > span - 2.0).sum()))
+                L.hc_diag_span(kspan, 0)   # kernel span and summed wave lifetimes (100 MHz)
+                ks = (kspan[1] - kspan[0]) * 1e-5
+                res.update(kernel_span_ms=round(ks, 3),
+                           first_dequeue_after_ms=round(((int(base) - kspan[0]) & 0xFFFFFFFF) * 1e-5, 3),
+                           wave_alive_frac=round(kspan[2] / max(1, kspan[3]) * 1e-5 / ks, 4))
             print(json.dumps(res), flush=True)
     L.hc_ab_set_path_order(None)
 

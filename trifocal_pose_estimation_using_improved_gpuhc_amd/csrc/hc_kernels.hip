@@ -332,6 +332,11 @@ __device__ __forceinline__ int2 score_half(const cf *sx, const float *edgels, in
     return make_int2(half_sum_i(c21), half_sum_i(c31));
 }
 
+#ifdef HC_DIAG_TIMES
+// diagnostic build: [0] first wave start, [1] last wave exit (s_memrealtime),
+// [2] summed wave lifetimes, [3] waves
+__device__ unsigned long long g_diag_span[4] = {~0ull, 0ull, 0ull, 0ull};
+#endif
 #ifdef HC_DIAG_PHASES
 // diagnostic build: per-phase shader cycles summed over waves (k_track):
 // [0] slot phases, [1] park + p(t), [2] dH/dx, [3] dH/dt | H, [5] LU,
@@ -396,6 +401,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     unsigned found_seen = 0u;   // abort mode: the found flag as of the last stage
 #ifdef HC_DIAG_TIMES
     int diag_t0 = 0;
+    const unsigned long long diag_w0 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0) atomicMin(&g_diag_span[0], diag_w0);
 #endif
     int s = 0, stepidx = 0, coef = 1, succ = 0, nsteps = 0, ncorr = 0;
     int piece = 0;   // steps since the path (re)started on this slot (time slicing)
@@ -769,6 +776,14 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             }
         }
     }
+#ifdef HC_DIAG_TIMES
+    if (lane == 0) {
+        const unsigned long long w1 = __builtin_amdgcn_s_memrealtime();
+        atomicMax(&g_diag_span[1], w1);
+        atomicAdd(&g_diag_span[2], w1 - diag_w0);
+        atomicAdd(&g_diag_span[3], 1ull);
+    }
+#endif
 #ifdef HC_DIAG_PHASES
     HC_DIAG_MARK(0);
     if (lane == 0) {
@@ -1126,6 +1141,16 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
 
 const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
 
+#ifdef HC_DIAG_TIMES
+int hc_diag_span(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_span), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[4] = {~0ull, 0ull, 0ull, 0ull};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_span), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 #ifdef HC_AB_PATH_ORDER
 // experiment build only: dequeue order = order[q] (a device array of the
 // launch's path ids, or null for the built-in order)
