@@ -114,27 +114,31 @@ def main():
     # RANSAC batches; a stream reuses its buffers only after its previous launch)
     NS = max(1, args.streams)
     NP = max(NS, args.pipelined_streams)
-    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(NP - 1)]
+    # the serial leg runs on the current stream; the pipelined leg on streams of
+    # its own (all non-default: the legacy default stream would order itself
+    # against them)
+    streams = [stream] + [torch.cuda.Stream(dev) for _ in range(NS - 1)]
+    pstreams = [torch.cuda.Stream(dev) for _ in range(args.pipelined_streams)]
     bufs = [res] + [tr.allocate(S, stats=True) for _ in range(NP - 1)]
     wss = [tr.new_workspace(S) for _ in range(NP)]
 
-    def step(i, ns):
+    def step(i, ns, strs):
         k = i % ns
-        with torch.cuda.stream(streams[k]):
+        with torch.cuda.stream(strs[k]):
             tr.reset_tracks(bufs[k])
-        tr.launch(tgt, dif, bufs[k], stream=streams[k], workspace=wss[k])
+        tr.launch(tgt, dif, bufs[k], stream=strs[k], workspace=wss[k])
 
-    def timed(ns):
+    def timed(ns, strs):
         """W untimed warmup steps, then K steps bracketed by barrier + sync; max over ranks."""
         for i in range(args.warmup):
-            step(i, ns)
+            step(i, ns, strs)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for i in range(args.steps):
-            step(i, ns)
+            step(i, ns, strs)
         torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
@@ -149,8 +153,8 @@ def main():
             el = float(tt.item())
         return el
 
-    elapsed = timed(NS)
-    pipe_elapsed = timed(args.pipelined_streams) if args.pipelined_streams > 1 else None
+    elapsed = timed(NS, streams)
+    pipe_elapsed = timed(args.pipelined_streams, pstreams) if args.pipelined_streams > 1 else None
 
     # kernel time of one launch alone (serial, HIP events on the launch stream): the
     # roofline's denominator and the latency of one batch

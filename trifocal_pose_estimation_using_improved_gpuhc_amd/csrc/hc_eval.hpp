@@ -87,6 +87,9 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
 #define HC_EV_AHEAD 2
 #endif
 constexpr int EV_AHEAD = HC_EV_AHEAD;
+#ifndef HC_GATHER_BFE
+#define HC_GATHER_BFE 1
+#endif
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
 struct HxOps { pf2 pa, pb, xu, xv; };
@@ -138,11 +141,22 @@ __device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const u
     // of the path loop (30 VGPRs held across the LU, then spilled)
     uint32_t m[3] = {map[0], map[1], map[2]};
     asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]));
+#if HC_GATHER_BFE
+    // slot = v_bfe_u32, address = v_lshl_add_u32 (2 VALU per column, not 3)
+    const char *eb = reinterpret_cast<const char *>(ent_row);
+#pragma unroll
+    for (int c = 0; c < NV; c++) {
+        uint32_t code;   // asm: the compiler would turn bfe + shift back into shift + and + add
+        asm("v_bfe_u32 %0, %1, %2, 3" : "=v"(code) : "v"(m[c / 10]), "i"(3 * (c % 10)));
+        rA[c] = *reinterpret_cast<const cf *>(eb + (code << 3));
+    }
+#else
 #pragma unroll
     for (int c = 0; c < NV; c++) {
         const uint32_t code = (m[c / 10] >> (3 * (c % 10))) & 7u;
         rA[c] = ent_row[code];
     }
+#endif
 }
 
 struct HtOps { pf2 pa, pb, da, db, xu, xv, xw; };

@@ -1160,8 +1160,8 @@ int hc_ab_set_path_order(const int *order) {
 #endif
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.1 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
-           "readlane back substitution, pipelined evals, 5 waves/SIMD, queue-position issue priority)";
+    return "hc_trifocal gfx950 v9.2 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
+           "readlane back substitution, pipelined evals, 5 waves/SIMD, time slicing at step boundaries)";
 }
 
 }  // extern "C"
