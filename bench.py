@@ -88,10 +88,18 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # rehearsal of the N>1 path on a one-GPU box (never set by the driver):
+    # HC_BENCH_DEVICE pins every rank to one device, HC_BENCH_BACKEND=gloo
+    # replaces RCCL (which refuses two ranks on one GPU)
+    dev_idx = int(os.environ.get("HC_BENCH_DEVICE", local_rank))
+    backend = os.environ.get("HC_BENCH_BACKEND", "nccl")
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     from trifocal_pose_estimation_using_improved_gpuhc_amd import (_abi, load_problem, load_ransac_data,
                                                                    prepare_target_params)
@@ -130,7 +138,7 @@ def main():
 
     def timed(ns, strs):
         """W untimed warmup steps, then K steps bracketed by barrier + sync; max over ranks."""
-        for i in range(args.warmup):
+        for i in range(max(args.warmup, ns)):   # every stream warm (its first launch pays for queue setup)
             step(i, ns, strs)
         torch.cuda.synchronize(dev)
         if world > 1:

@@ -1,6 +1,7 @@
 """Concurrent launches of the sliced vs unsliced tracker on 1/2/4 streams
 (config 2 batches, own buffers and workspace per stream): wall ms per batch.
-Usage: python scripts/stream_probe.py OUT.jsonl"""
+Usage: python scripts/stream_probe.py OUT.jsonl [STREAMS,...]
+(run two copies at once to see launches of two processes on one GPU)"""
 import json
 import sys
 import time
@@ -21,7 +22,7 @@ dif = torch.from_numpy(dif_np).to(dev)
 tr = DeviceTracker(problem, dev)
 out = open(sys.argv[1], "w")
 for sliced in (True, False):
-    for ns in (1, 2, 4):
+    for ns in (tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (1, 2, 4)):
         streams = [torch.cuda.Stream(dev) for _ in range(ns)]
         bufs = [tr.allocate(S) for _ in range(ns)]
         wss = [tr.new_workspace(S if sliced else 0) for _ in range(ns)]
