@@ -105,6 +105,9 @@ static_assert(sizeof(PathState) == 32, "PathState is 32 bytes");
 #define HC_SLICE_Q 3
 #endif
 constexpr int SLICE_Q = HC_SLICE_Q;          // steps per time slice (0: no slicing)
+#ifndef HC_PRIO_LAS
+#define HC_PRIO_LAS 1
+#endif
 constexpr unsigned RING_SLACK = 1u << 16;    // ring entries beyond one per path (> 2x the path slots)
 
 struct KArgs {
@@ -336,6 +339,13 @@ __device__ __forceinline__ int2 score_half(const cf *sx, const float *edgels, in
 // diagnostic build: [0] first wave start, [1] last wave exit (s_memrealtime),
 // [2] summed wave lifetimes, [3] waves
 __device__ unsigned long long g_diag_span[4] = {~0ull, 0ull, 0ull, 0ull};
+#ifdef HC_DIAG_UTIL
+// diagnostic build (with HC_DIAG_TIMES): per 10.24-us bin of s_memrealtime
+// (modulo 8192 bins = 84 ms), the path-stages and the wave-stages started
+// (64 copies of each bin, picked by workgroup, so the atomics do not serialise)
+constexpr int UTIL_BINS = 8192, UTIL_COPIES = 64;
+__device__ unsigned long long g_diag_util[UTIL_COPIES][UTIL_BINS][2];
+#endif
 #endif
 #ifdef HC_DIAG_PHASES
 // diagnostic build: per-phase shader cycles summed over waves (k_track):
@@ -627,6 +637,17 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
         }
         if (__ballot(ph == PH_STAGE) == 0ull) break;
+#ifdef HC_DIAG_UTIL
+        {
+            const unsigned long long bs = __ballot(ph == PH_STAGE);
+            if (lane == 0) {
+                const unsigned bin = (unsigned)(__builtin_amdgcn_s_memrealtime() >> 10) & (UTIL_BINS - 1);
+                unsigned long long *u = g_diag_util[blockIdx.x % UTIL_COPIES][bin];
+                atomicAdd(&u[0], (unsigned long long)((bs & 1ull) + ((bs >> 32) & 1ull)));
+                atomicAdd(&u[1], 1ull);
+            }
+        }
+#endif
         if (!ABORT && a.ordered && a.slice_q == 0) {
             // Without time slicing: issue priority by queue position (s_setprio,
             // arbitration among the waves of a SIMD): the last tenth of the
@@ -642,6 +663,22 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             else if (lvl >= PRIO_TENTHS - 3) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
+#if HC_PRIO_LAS
+        if (!ABORT && a.slice_q > 0) {
+            // With time slicing: issue priority to the wave whose paths have
+            // run the fewest steps (least attained service): a path's remaining
+            // steps are bounded by max_steps - stepidx, so the paths that can
+            // still run longest get the larger share of their SIMD, and the
+            // launch ends with evenly short remainders.
+            const int si = (ph == PH_STAGE) ? stepidx : (1 << 20);
+            const int m = min(__builtin_amdgcn_readlane(si, 0), __builtin_amdgcn_readlane(si, 32));
+            const int q4 = (int)((long long)m * 4 / (a.max_steps + 1));
+            if (q4 <= 0) __builtin_amdgcn_s_setprio(3);
+            else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
+            else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
         HC_DIAG_MARK(0);
         // the found flag for the next step boundary: read now, used after the stage
         if (ABORT && a.inflight_stop) found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1151,6 +1188,17 @@ int hc_diag_span(unsigned long long *out, int reset) {
     return 0;
 }
 #endif
+#ifdef HC_DIAG_UTIL
+int hc_diag_util(unsigned long long *out, int reset) {
+    const size_t n = sizeof(unsigned long long) * 2 * hc::UTIL_BINS * hc::UTIL_COPIES;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_util), n) != hipSuccess) return -1;
+    if (reset) {
+        void *p = nullptr;
+        if (hipGetSymbolAddress(&p, HIP_SYMBOL(hc::g_diag_util)) != hipSuccess || hipMemset(p, 0, n) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 #ifdef HC_AB_PATH_ORDER
 // experiment build only: dequeue order = order[q] (a device array of the
 // launch's path ids, or null for the built-in order)
@@ -1161,7 +1209,8 @@ int hc_ab_set_path_order(const int *order) {
 
 const char *hc_trifocal_version(void) {
     return "hc_trifocal gfx950 v9.2 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
-           "readlane back substitution, pipelined evals, 5 waves/SIMD, time slicing at step boundaries)";
+           "readlane back substitution, pipelined evals, 5 waves/SIMD, time slicing at step boundaries with "
+           "least-attained-service issue priority)";
 }
 
 }  // extern "C"
