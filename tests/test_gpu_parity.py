@@ -4,6 +4,7 @@ Bar: identical values -- the kernel and the oracle implement the sam
 op-level spec, so every float must match exactly, treating +0 == -0 and
 NaN == NaN; converged / infinity flags and step / correction counts identical.
 """
+import ctypes
 import os
 
 import numpy as np
@@ -175,6 +176,33 @@ def test_time_slicing_is_bit_exact(problem, samples100, tracker):
     assert np.array_equal(a["stats"]["steps"], b["stats"]["steps"])
     assert np.array_equal(a["stats"]["corrections"], b["stats"]["corrections"])
     assert np.array_equal(a["tracks"].view(np.uint32), b["tracks"].view(np.uint32))
+
+
+def test_time_slicing_concurrent_streams(problem, samples100, tracker):
+    """Four sliced launches in flight at once on four streams (own buffers and
+    workspaces, the bench's pipelined leg): the suspend / resume hand-over of
+    each launch stays inside its own workspace, and every launch equals the
+    serial run bit for bit."""
+    import torch
+    tgt, dif, _ = samples100
+    ref = tracker.track(tgt, dif).host()
+    dev = tracker.device
+    t, d = torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev)
+    streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    bufs = [tracker.allocate(tgt.shape[0]) for _ in range(4)]
+    wss = [tracker.new_workspace(tgt.shape[0]) for _ in range(4)]
+    torch.cuda.synchronize(dev)
+    for k in range(4):
+        with torch.cuda.stream(streams[k]):
+            tracker.reset_tracks(bufs[k])
+        tracker.launch(t, d, bufs[k], stream=streams[k], workspace=wss[k])
+    torch.cuda.synchronize(dev)
+    for k in range(4):
+        h = bufs[k].host()
+        assert int(tracker.L.hc_trifocal_workspace_status(ctypes.c_void_p(wss[k].data_ptr()))) == 0
+        assert (h["converge"] == ref["converge"]).all() and (h["infinity"] == ref["infinity"]).all()
+        assert np.array_equal(h["stats"]["steps"], ref["stats"]["steps"])
+        assert np.array_equal(h["tracks"].view(np.uint32), ref["tracks"].view(np.uint32))
 
 
 def test_tracker_abort_mode(problem, samples100, tracker):
