@@ -117,14 +117,21 @@ typedef struct {
 size_t hc_trifocal_workspace_size(void);
 
 /* Workspace size that also enables time slicing for launches of up to
-   sub_ransac_iters samples: 32 + 8 bytes per path more (suspended paths'
-   step-control state and the resume ring).  With it, a path that has run a
+   sub_ransac_iters samples at GPUHC_Max_Steps = 80: 32 + 8 x 28 bytes per path
+   more (suspended paths' step-control state and the resume ring, one entry
+   per suspension).  With it, a path that has run a
    slice of steps while other paths wait is suspended at a step boundary and
    resumed after the new paths (same results bit for bit; every path starts
    early, so a launch no longer ends with long paths that were dequeued late).
    Tracking launches only (not abort mode).  A smaller workspace of at least
    hc_trifocal_workspace_size() runs without slicing. */
 size_t hc_trifocal_workspace_size_for(int sub_ransac_iters);
+
+/* The same for a given GPUHC_Max_Steps (hc_trifocal_workspace_size_for assumes
+   the reference default, 80): the suspended-path ring holds one entry per
+   suspension, at most (max_steps + 1) / 3 per path.  A workspace sized for a
+   smaller max_steps than a launch uses runs that launch without slicing. */
+size_t hc_trifocal_workspace_size_for_steps(int sub_ransac_iters, int max_steps);
 
 /* GPU-HC tracking of 312*N paths (replaces ..._TrunPaths and ..._TrunPaths_Volta). */
 hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace,

@@ -43,15 +43,15 @@ struct StreamState {
 };
 
 // the stream's workspace, grown to time-slicing size for launches of N samples
-// (hc_trifocal_workspace_size_for; N = 0: abort mode, the base size)
-StreamState *state_for(hipStream_t s, bool need_unified, int N = 0) {
+// (hc_trifocal_workspace_size_for_steps; N = 0: abort mode, the base size)
+StreamState *state_for(hipStream_t s, bool need_unified, int N = 0, int max_steps = 80) {
     static std::mutex mu;
     static std::map<std::pair<int, hipStream_t>, StreamState> states;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(mu);
     StreamState &st = states[{dev, s}];
-    const size_t need = N > 0 ? hc_trifocal_workspace_size_for(N) : hc_trifocal_workspace_size();
+    const size_t need = N > 0 ? hc_trifocal_workspace_size_for_steps(N, max_steps) : hc_trifocal_workspace_size();
     if (st.workspace && st.ws_bytes < need) {
         // the previous launch on this stream may still use it
         if (hipStreamSynchronize(s) != hipSuccess || hipFree(st.workspace) != hipSuccess) return nullptr;
@@ -105,7 +105,7 @@ real_Double_t track(magma_queue_t q, int N, int max_steps, int max_corr, int inc
                     const int *unified, const int *d_hx, const int *d_ht, bool *conv, bool *inf, const char *name,
                     bool truncate = true, bool explicit_rk = false) {
     hipStream_t s = magma_queue_get_hip_stream(q);
-    StreamState *st = state_for(s, unified == nullptr, N);
+    StreamState *st = state_for(s, unified == nullptr, N, max_steps);
     if (!st) { report(HC_ERROR_WORKSPACE, name); return 0.0; }
     const int32_t *U = unified ? reinterpret_cast<const int32_t *>(unified) : unify(st, d_hx, d_ht, s);
     if (!U) { report(HC_ERROR_LAUNCH, name); return 0.0; }

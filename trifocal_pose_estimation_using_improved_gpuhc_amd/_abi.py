@@ -84,6 +84,8 @@ def lib() -> C.CDLL:
         L.hc_trifocal_workspace_size.restype = C.c_size_t
         L.hc_trifocal_workspace_size_for.restype = C.c_size_t
         L.hc_trifocal_workspace_size_for.argtypes = [C.c_int]
+        L.hc_trifocal_workspace_size_for_steps.restype = C.c_size_t
+        L.hc_trifocal_workspace_size_for_steps.argtypes = [C.c_int, C.c_int]
         L.hc_trifocal_version.restype = C.c_char_p
         L.hc_last_error_string.restype = C.c_char_p
         for fn in ("hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
@@ -135,7 +137,7 @@ def check(status: int, what: str) -> None:
 
 # Exported symbols that include/*.h declare (tests check the library exports all of them).
 DECLARED_SYMBOLS = (
-    "hc_trifocal_workspace_size", "hc_trifocal_workspace_size_for", "hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
+    "hc_trifocal_workspace_size", "hc_trifocal_workspace_size_for", "hc_trifocal_workspace_size_for_steps", "hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
     "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
     "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
     "hc_last_error_string",

@@ -165,8 +165,8 @@ void GPU_HC_Solver::Allocate_Arrays() {
     h_diffParams.assign((size_t)Num_Of_RANSAC_Iterations * NPP * 2, 0.0f);
     h_picked.assign((size_t)Num_Of_RANSAC_Iterations * 3, 0);
     for (PerGPU *p : gpus_) {
-        // room for time slicing of this GPU's tracking launch (hc_trifocal_workspace_size_for)
-        const size_t wsb = hc_trifocal_workspace_size_for(p->N);
+        // room for time slicing of this GPU's tracking launch (hc_trifocal_workspace_size_for_steps)
+        const size_t wsb = hc_trifocal_workspace_size_for_steps(p->N, GPUHC_Max_Steps);
         HC_HIP_CHECK(hipSetDevice(p->dev));
         const size_t n = (size_t)NT * p->N;
         HC_HIP_CHECK(hipMalloc(&p->d_Start_Sols, (size_t)NT * (NV + 1) * sizeof(hcComplex)));

@@ -90,6 +90,9 @@ constexpr int EV_AHEAD = HC_EV_AHEAD;
 #ifndef HC_GATHER_BFE
 #define HC_GATHER_BFE 1
 #endif
+#ifndef HC_EV_SCHED
+#define HC_EV_SCHED 2
+#endif
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
 struct HxOps { pf2 pa, pb, xu, xv; };
@@ -120,6 +123,9 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
         const bool last = (int)w[k].y < 0;   // last term of an entry (never set on padding terms)
         *reinterpret_cast<pf2 *>(eb + (last ? ((w[k].y >> 24) & 0x7Fu) : 8u * 6u)) = acc;
         acc = last ? pf2{0.0f, 0.0f} : acc;
+#if HC_EV_SCHED >= 2
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 }
 
@@ -186,6 +192,9 @@ __device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r
         s = s * pf2{co, co};
         const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
         acc = pcmsub(acc, P, q.xw);
+#if HC_EV_SCHED
+        __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
+#endif
     }
     return cmk(acc.x, acc.y);
 }
@@ -215,6 +224,9 @@ __device__ __forceinline__ cf eval_h(const uint2 *s_ht, const SlotLDS &S, int r)
         pf2 P = q.pa * pf2{co, co};
         P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
         acc = pcmadd(acc, P, q.xw);
+#if HC_EV_SCHED
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     return cmk(acc.x, acc.y);
 }

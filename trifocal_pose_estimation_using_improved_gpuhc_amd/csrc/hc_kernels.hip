@@ -72,7 +72,8 @@ struct Workspace {
     unsigned pad0;
     unsigned long long t_start;   // s_memrealtime when the first workgroup started (abort mode)
     unsigned long long t_found;   // s_memrealtime of the first good hypothesis
-    unsigned pad1[8];
+    unsigned ring_fail[4];   // time slicing: ticket, tag seen, tail, head of a ring entry that never came (diagnostics)
+    unsigned pad1[4];
     // written by k_prep_tables
     EvalTables tab;
 };
@@ -108,7 +109,20 @@ constexpr int SLICE_Q = HC_SLICE_Q;          // steps per time slice (0: no slic
 #ifndef HC_PRIO_LAS
 #define HC_PRIO_LAS 1
 #endif
-constexpr unsigned RING_SLACK = 1u << 16;    // ring entries beyond one per path (> 2x the path slots)
+// Ring: one entry per ticket, never reused within a launch.  A path is
+// suspended only after running SLICE_Q steps since it (re)started and runs at
+// most max_steps + 1 steps, so a launch pushes at most
+// paths * ((max_steps + 1) / SLICE_Q) entries.  (A reused slot is not safe: a
+// wave can be paused for hundreds of ms between taking a ticket and reading
+// its entry while the rest of its kernel runs on -- seen when another stream's
+// first launch created its hardware queue -- and a slot reused meanwhile would
+// lose the suspended path; profiles/r2zb_stress*.jsonl.)
+__host__ __device__ constexpr unsigned long long ring_entries(long long paths, int max_steps) {
+    return (unsigned long long)paths * (unsigned long long)((max_steps + 1) / (SLICE_Q > 0 ? SLICE_Q : 1) + 1) + 64ull;
+}
+// the longest a consumer waits for a claimed entry whose pusher holds its
+// ticket but has not written it yet (s_memrealtime ticks, 100 MHz: 10 s)
+constexpr unsigned long long RING_WAIT_TICKS = 1000000000ull;
 
 struct KArgs {
     int num_paths;
@@ -146,22 +160,26 @@ constexpr int RQ_HEAD = 0, RQ_TAIL = 64, RQ_AVAIL = 128, RQ_WORDS = 192;
 __device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// the hand-over data of a suspended path is written and read with agent-scope
-// relaxed atomics (coherent across the XCDs' L2s without cache-wide fences);
-// the writer drains its stores (s_waitcnt vmcnt(0)) before publishing the ring
-// entry, and the reader's loads depend on the entry's path id
+// The hand-over data of a suspended path (x, PathState, ring entries) is
+// written and read with agent-scope relaxed atomics (coherent across the
+// XCDs' L2s without cache-wide fences); the writer drains its stores
+// (s_waitcnt vmcnt(0)) before publishing the ring entry, and the reader's
+// loads depend on the entry's path id.
+__device__ __forceinline__ void st_u64_h(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long ld_u64_h(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long pack2(unsigned lo, unsigned hi) {
+    return (unsigned long long)lo | ((unsigned long long)hi << 32);
+}
 __device__ __forceinline__ void st_cf_rlx(cf *p, cf v) {
-    __hip_atomic_store(reinterpret_cast<unsigned long long *>(p),
-                       (unsigned long long)__float_as_uint(v.x) | ((unsigned long long)__float_as_uint(v.y) << 32),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st_u64_h(reinterpret_cast<unsigned long long *>(p), pack2(__float_as_uint(v.x), __float_as_uint(v.y)));
 }
 __device__ __forceinline__ cf ld_cf_rlx(const cf *p) {
-    const unsigned long long u =
-        __hip_atomic_load(reinterpret_cast<const unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long u = ld_u64_h(reinterpret_cast<const unsigned long long *>(p));
     return cmk(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
-}
-__device__ __forceinline__ void st_i_rlx(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ int ld_i_rlx(const int *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -170,35 +188,56 @@ __device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F
 
 // (pointers and sizes by value: a KArgs reference would put the kernel
 // arguments in scratch memory)
-__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, int b, bool unpaired) {
+__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, int b, bool unpaired,
+                                          Workspace *ws) {
     const unsigned t = atomicAdd(&rq[RQ_TAIL], 1u);
-    __hip_atomic_store(&ring[t % cap], ((unsigned long long)(t + 1u) << 32) | (unsigned)b, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+    if (t >= cap) {   // cannot happen within the bound of ring_entries (the path would be lost: reported)
+        atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
+        return;
+    }
+    st_u64_h(&ring[t], ((unsigned long long)(t + 1u) << 32) | (unsigned)b);
     if (unpaired) {
         drain_stores();
         atomicAdd(&rq[RQ_AVAIL], 1u);
     }
 }
-// the entry of claimed ticket h (bounded wait; HC_ERROR_DEVICE in the status if it never comes)
-__device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigned cap, Workspace *ws, unsigned h) {
-    for (int spin = 0; spin < (1 << 22); spin++) {
-        const unsigned long long e = __hip_atomic_load(&ring[h % cap], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((unsigned)(e >> 32) == h + 1u) return (int)(unsigned)e;
-        __builtin_amdgcn_s_sleep(2);
+// the entry of claimed ticket h: its pusher took ticket h before (head never
+// passes tail), so it is written or about to be; a pusher paused mid-push is
+// waited for (bounded: HC_ERROR_DEVICE in the status if it never comes)
+__device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigned cap, Workspace *ws, unsigned h,
+                                         const unsigned *rq) {
+    if (h >= cap) {
+        atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
+        return -1;
     }
-    atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
+    unsigned long long e = ld_u64_h(&ring[h]);
+    if ((unsigned)(e >> 32) == h + 1u) return (int)(unsigned)e;
+    const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(8);
+        e = ld_u64_h(&ring[h]);
+        if ((unsigned)(e >> 32) == h + 1u) return (int)(unsigned)e;
+        if (__builtin_amdgcn_s_memrealtime() - w0 > RING_WAIT_TICKS) break;
+    }
+    if (atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE) == 0u) {
+        // diagnostics: ticket, tag seen, tail, head
+        ws->ring_fail[0] = h;
+        ws->ring_fail[1] = (unsigned)(e >> 32);
+        ws->ring_fail[2] = ld_rlx(&rq[RQ_TAIL]);
+        ws->ring_fail[3] = ld_rlx(&rq[RQ_HEAD]);
+    }
     return -1;
 }
 __device__ __forceinline__ int ring_pop_paired(unsigned *rq, const unsigned long long *ring, unsigned cap,
                                                Workspace *ws) {
-    return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u));
+    return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
 }
 // oldest suspended path id, or -1 if there is none
 __device__ __forceinline__ int ring_pop(unsigned *rq, const unsigned long long *ring, unsigned cap, Workspace *ws) {
     int *avail = reinterpret_cast<int *>(&rq[RQ_AVAIL]);
     if (ld_i_rlx(avail) <= 0) return -1;
     for (;;) {
-        if (atomicSub(avail, 1) > 0) return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u));
+        if (atomicSub(avail, 1) > 0) return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
         if (atomicAdd(avail, 1) + 1 <= 0) return -1;
     }
 }
@@ -504,14 +543,16 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     x = rl ? ld_cf_rlx(dtrack + r) : cmk(0.0f, 0.0f);
                     xl = x;
                     sols = x;
-                    const int *q = reinterpret_cast<const int *>(a.pst + b);
-                    t0 = __int_as_float(ld_i_rlx(q + 0));
-                    dt = __int_as_float(ld_i_rlx(q + 1));
-                    stepidx = ld_i_rlx(q + 2);
-                    nsteps = ld_i_rlx(q + 3);
-                    ncorr = ld_i_rlx(q + 4);
-                    succ = ld_i_rlx(q + 5);
-                    const int fl = ld_i_rlx(q + 6);
+                    const unsigned long long *q = reinterpret_cast<const unsigned long long *>(a.pst + b);
+                    const unsigned long long q0 = ld_u64_h(q + 0), q1 = ld_u64_h(q + 1), q2 = ld_u64_h(q + 2),
+                                             q3 = ld_u64_h(q + 3);
+                    t0 = __uint_as_float((unsigned)q0);
+                    dt = __uint_as_float((unsigned)(q0 >> 32));
+                    stepidx = (int)(unsigned)q1;
+                    nsteps = (int)(unsigned)(q1 >> 32);
+                    ncorr = (int)(unsigned)q2;
+                    succ = (int)(unsigned)(q2 >> 32);
+                    const int fl = (int)(unsigned)q3;
                     end_zone = (fl & 1) != 0; check = (fl & 2) != 0; isSucc = false; isInf = false;
                     t_step = 0.0f;
                     piece = 0;
@@ -601,17 +642,14 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
                         if (rl) st_cf_rlx(dtrack + r, x);
                         if (r == 0) {
-                            int *q = reinterpret_cast<int *>(a.pst + b);
-                            st_i_rlx(q + 0, __float_as_int(t0));
-                            st_i_rlx(q + 1, __float_as_int(dt));
-                            st_i_rlx(q + 2, stepidx);
-                            st_i_rlx(q + 3, nsteps);
-                            st_i_rlx(q + 4, ncorr);
-                            st_i_rlx(q + 5, succ);
-                            st_i_rlx(q + 6, (end_zone ? 1 : 0) | (check ? 2 : 0));
+                            unsigned long long *q = reinterpret_cast<unsigned long long *>(a.pst + b);
+                            st_u64_h(q + 0, pack2(__float_as_uint(t0), __float_as_uint(dt)));
+                            st_u64_h(q + 1, pack2((unsigned)stepidx, (unsigned)nsteps));
+                            st_u64_h(q + 2, pack2((unsigned)ncorr, (unsigned)succ));
+                            st_u64_h(q + 3, pack2((unsigned)((end_zone ? 1 : 0) | (check ? 2 : 0)), 0u));
                         }
                         drain_stores();
-                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, b, hint >= 0);
+                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, b, hint >= 0, ws);
                         deq_hint = hint;
                         suspend = true;
                     } else {
@@ -933,10 +971,12 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
 // ---------------------------------------------------------------- host side
 static size_t ws_bytes_needed() { return (sizeof(Workspace) + 255) & ~(size_t)255; }
 // + the time-slicing area of a launch of `paths` paths: PathState per path, then the ring
-static size_t ws_bytes_for(long long paths) {
+static size_t ws_bytes_for(long long paths, int max_steps) {
     if (paths < 0) paths = 0;
+    if (max_steps < 0) max_steps = 0;
     return ws_bytes_needed() + ((RQ_WORDS * sizeof(unsigned) + (size_t)paths * sizeof(PathState) +
-                                 ((size_t)paths + RING_SLACK) * sizeof(unsigned long long) + 255) & ~(size_t)255);
+                                 (size_t)ring_entries(paths, max_steps) * sizeof(unsigned long long) + 255) &
+                                ~(size_t)255);
 }
 
 // Persistent grid: resident workgroups (occupancy API, cached per device and
@@ -1010,12 +1050,13 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.stats = t->stats;
     k.ws = ws;
     // time slicing when the workspace has room for it (hc_trifocal_workspace_size_for)
-    if (!abort_mode && SLICE_Q > 0 && wsb >= ws_bytes_for(paths)) {
+    if (!abort_mode && SLICE_Q > 0 && wsb >= ws_bytes_for(paths, t->settings.max_steps) &&
+        ring_entries(paths, t->settings.max_steps) < 0xFFFFFF00ull) {
         char *base = (char *)workspace + ws_bytes_needed();
         k.rq = (unsigned *)base;
         k.pst = (PathState *)(base + RQ_WORDS * sizeof(unsigned));
         k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) + (size_t)paths * sizeof(PathState));
-        k.ring_cap = (unsigned)(paths + RING_SLACK);
+        k.ring_cap = (unsigned)ring_entries(paths, t->settings.max_steps);
         k.slice_q = SLICE_Q;
         // counters + ring zeroed (sequence tags of an earlier launch never match)
         if ((g_last_hip_error = hipMemsetAsync(k.rq, 0, RQ_WORDS * sizeof(unsigned), s)) != hipSuccess ||
@@ -1088,7 +1129,11 @@ int hc_diag_luwork(unsigned long long *out, int reset) {
 size_t hc_trifocal_workspace_size(void) { return hc::ws_bytes_needed(); }
 
 size_t hc_trifocal_workspace_size_for(int sub_ransac_iters) {
-    return hc::ws_bytes_for(sub_ransac_iters > 0 ? (long long)sub_ransac_iters * hc::NTRK : 0);
+    return hc_trifocal_workspace_size_for_steps(sub_ransac_iters, 80);
+}
+
+size_t hc_trifocal_workspace_size_for_steps(int sub_ransac_iters, int max_steps) {
+    return hc::ws_bytes_for(sub_ransac_iters > 0 ? (long long)sub_ransac_iters * hc::NTRK : 0, max_steps);
 }
 
 hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace, size_t workspace_bytes,

@@ -124,7 +124,7 @@ class DeviceTracker:
             raise _abi.HCError("sample range outside the buffers")
         p0, p1 = sample_offset * 312, (sample_offset + num_samples) * 312
         if workspace is None and not abort and time_slicing:
-            need = int(self.L.hc_trifocal_workspace_size_for(num_samples))
+            need = int(self.L.hc_trifocal_workspace_size_for_steps(num_samples, self.settings.max_steps))
             if self.workspace.numel() < need:
                 self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
         ws_t = workspace if workspace is not None else self.workspace
@@ -177,7 +177,8 @@ class DeviceTracker:
     def new_workspace(self, num_samples: int = 0) -> torch.Tensor:
         """A workspace; with num_samples > 0, large enough for time slicing of
         tracking launches of up to that many samples."""
-        n = int(self.L.hc_trifocal_workspace_size_for(num_samples)) if num_samples > 0 else self.ws_bytes
+        n = (int(self.L.hc_trifocal_workspace_size_for_steps(num_samples, self.settings.max_steps))
+             if num_samples > 0 else self.ws_bytes)
         return torch.zeros(n, dtype=torch.uint8, device=self.device)
 
     def launch_abort_chunked(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, chunk_samples: int,
