@@ -151,6 +151,11 @@ def main():
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
+        import ctypes
+        for k in range(ns):   # a suspended path the time-slicing ring failed to hand over would show here
+            st = int(tr.L.hc_trifocal_workspace_status(ctypes.c_void_p(wss[k].data_ptr())))
+            if st != 0:
+                raise RuntimeError(f"workspace {k}: status {st}")
         for k in range(1, min(ns, args.steps)):   # every batch is the same work: identical results on every stream
             if not (torch.equal(bufs[k].converge, res.converge) and torch.equal(bufs[k].stats, res.stats)
                     and torch.equal(bufs[k].tracks, res.tracks)):
