@@ -109,6 +109,9 @@ constexpr int SLICE_Q = HC_SLICE_Q;          // steps per time slice (0: no slic
 #ifndef HC_PRIO_LAS
 #define HC_PRIO_LAS 1
 #endif
+#ifndef HC_PRIO_ABORT
+#define HC_PRIO_ABORT 1
+#endif
 // Ring: one entry per ticket, never reused within a launch.  A path is
 // suspended only after running SLICE_Q steps since it (re)started and runs at
 // most max_steps + 1 steps, so a launch pushes at most
@@ -684,6 +687,24 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                 atomicAdd(&u[0], (unsigned long long)((bs & 1ull) + ((bs >> 32) & 1ull)));
                 atomicAdd(&u[1], 1ull);
             }
+        }
+#endif
+#if HC_PRIO_ABORT
+        if (ABORT) {
+            // Abort mode: first come, first served.  The queue is sample-major,
+            // so the waves holding the earliest hypotheses get the higher issue
+            // priority (the first sixteenth of the launch's paths at 3, the next
+            // at 2, the next at 1) and whole early hypotheses complete -- and are
+            // scored -- sooner, instead of every hypothesis in flight
+            // progressing at the same rate.  Which paths are tracked, and their
+            // results, do not depend on it (only on when the pose flag is set).
+            const int qp = (ph == PH_STAGE) ? qpos : 0x7FFFFFFF;
+            const int m = min(__builtin_amdgcn_readlane(qp, 0), __builtin_amdgcn_readlane(qp, 32));
+            const int lvl = (int)((long long)m * 16 / a.num_paths);
+            if (lvl <= 0) __builtin_amdgcn_s_setprio(3);
+            else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
+            else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
         }
 #endif
         if (!ABORT && a.ordered && a.slice_q == 0) {
