@@ -26,7 +26,32 @@ namespace hc {
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
+#ifndef HC_HX_GROUPED
+#define HC_HX_GROUPED 1
+#endif
+#if HC_HX_GROUPED
+// dH/dx terms grouped by entry: a row's entries sorted by their number of
+// terms (largest first) go to entry slots 0..5, slot s holding at most
+// HX_GCAP[s] terms (this problem's maxima over the rows: 8, 5, 5, 5, 1, 1).
+// Every lane's entries then end at the same static term positions, so the
+// term loop stores each entry once, at compile-time positions, instead of a
+// running sum per term (6 stores instead of 24, no per-term address or reset
+// selects).  Shorter entries are padded with coefficient-0 terms on unit
+// operands (p[33] = x[30] = 1), as the reference pads its 8-term lists.
+constexpr int HX_GCAP[6] = {8, 5, 5, 5, 1, 1};
+constexpr int HX_SLOT_CAP = 25;
+__host__ __device__ constexpr int hx_gend(int s) { return s < 0 ? 0 : hx_gend(s - 1) + HX_GCAP[s]; }   // end of slot s
+__host__ __device__ constexpr bool hx_is_gend(int k) {
+    return k + 1 == hx_gend(0) || k + 1 == hx_gend(1) || k + 1 == hx_gend(2) || k + 1 == hx_gend(3) ||
+           k + 1 == hx_gend(4) || k + 1 == hx_gend(5);
+}
+__host__ __device__ constexpr int hx_gslot(int k) {
+    return k < hx_gend(0) ? 0 : k < hx_gend(1) ? 1 : k < hx_gend(2) ? 2 : k < hx_gend(3) ? 3 : k < hx_gend(4) ? 4 : 5;
+}
+static_assert(hx_gend(5) == HX_SLOT_CAP, "slot capacities");
+#else
 constexpr int HX_SLOT_CAP = 24;   // per-lane dH/dx terms (this problem: 23)
+#endif
 constexpr int SLOT_OFF_X = (int)offsetof(SlotLDS, x);
 constexpr int SLOT_OFF_P = (int)offsetof(SlotLDS, p);
 constexpr int SLOT_DIF_DELTA = (int)offsetof(SlotLDS, dif) - (int)offsetof(SlotLDS, p);
@@ -120,9 +145,16 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
         P = pcmul(P, q.pb);
         P = pcmul(P, q.xu);
         acc = pcmadd(acc, P, q.xv);
+#if HC_HX_GROUPED
+        if (hx_is_gend(k)) {                 // static: the entry of slot hx_gslot(k) ends here on every lane
+            if (r < NV) *reinterpret_cast<pf2 *>(eb + 8 * hx_gslot(k)) = acc;   // (padding lanes alias row 0)
+            acc = pf2{0.0f, 0.0f};
+        }
+#else
         const bool last = (int)w[k].y < 0;   // last term of an entry (never set on padding terms)
         *reinterpret_cast<pf2 *>(eb + (last ? ((w[k].y >> 24) & 0x7Fu) : 8u * 6u)) = acc;
         acc = last ? pf2{0.0f, 0.0f} : acc;
+#endif
 #if HC_EV_SCHED >= 2
         __builtin_amdgcn_sched_barrier(0);
 #endif

@@ -270,6 +270,56 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
         bool bad = false;
         uint32_t map[3] = {0u, 0u, 0u};
         for (int c = 0; c < NV; c++) map[c / 10] |= 6u << (3 * (c % 10));
+#if HC_HX_GROUPED
+        // entries sorted by their number of non-zero terms, largest first (ties:
+        // lower column first); entry s fills slot s's HX_GCAP[s] term words,
+        // padded with coefficient-0 terms
+        for (int k2 = 0; k2 < HX_SLOT_CAP; k2++) T->hx[k2 * 32 + r] = pad_hx;
+        if (r < NV) {
+            // slot capacities and starts as locals (a runtime index into the
+            // namespace-scope constexpr table does not reach device memory)
+            int cap[6], start[6];
+            for (int s2 = 0, acc2 = 0; s2 < 6; s2++) {
+                cap[s2] = HX_GCAP[0] * (s2 == 0) + HX_GCAP[1] * (s2 == 1) + HX_GCAP[2] * (s2 == 2) +
+                          HX_GCAP[3] * (s2 == 3) + HX_GCAP[4] * (s2 == 4) + HX_GCAP[5] * (s2 == 5);
+                start[s2] = acc2;
+                acc2 += cap[s2];
+            }
+            int cnt[NV];
+            for (int c = 0; c < NV; c++) {
+                cnt[c] = 0;
+                for (int j = 0; j < HX_TERMS; j++)
+                    if (U[(c * HX_TERMS + j) * HX_PARTS * NV + r] != 0) cnt[c]++;
+            }
+            for (;;) {
+                int best = -1;
+                for (int c = 0; c < NV; c++)
+                    if (cnt[c] > 0 && (best < 0 || cnt[c] > cnt[best])) best = c;
+                if (best < 0) break;
+                const int c = best;
+                if (slot >= 6 || cnt[c] > cap[slot]) { bad = true; break; }
+                int pos = start[slot];
+                for (int j = 0; j < HX_TERMS; j++) {
+                    const int base = (c * HX_TERMS + j) * HX_PARTS * NV + r;
+                    const int co = U[base], a = U[base + NV], b = U[base + 2 * NV], u = U[base + 3 * NV],
+                              v = U[base + 4 * NV];
+                    if (co == 0) continue;
+                    bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
+                           v < 0 || v > NV;
+                    if (!bad)
+                        T->hx[pos * 32 + r] = make_uint2(
+                            (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
+                            (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
+                                (((uint32_t)co & 0xFFu) << 16));
+                    pos++;
+                    n++;
+                }
+                map[c / 10] = (map[c / 10] & ~(7u << (3 * (c % 10)))) | ((uint32_t)slot << (3 * (c % 10)));
+                cnt[c] = 0;
+                slot++;
+            }
+        }
+#else
         if (r < NV) {
             for (int c = 0; c < NV; c++) {
                 int last_j = -1;
@@ -295,8 +345,11 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
                 slot++;
             }
         }
+#endif
         if (n > HX_SLOT_CAP) bad = true;
+#if !HC_HX_GROUPED
         for (int k2 = n; k2 < HX_SLOT_CAP; k2++) T->hx[k2 * 32 + r] = pad_hx;
+#endif
         for (int q = 0; q < 3; q++) T->map[q][r] = map[q];
         s_len[r] = n;
         const int32_t *D = U + HX_SIZE;
