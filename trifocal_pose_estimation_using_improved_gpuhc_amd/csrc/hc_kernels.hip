@@ -1327,9 +1327,9 @@ int hc_ab_set_path_order(const int *order) {
 #endif
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.2 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
-           "readlane back substitution, pipelined evals, 5 waves/SIMD, time slicing at step boundaries with "
-           "least-attained-service issue priority)";
+    return "hc_trifocal gfx950 v9.3 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
+           "readlane back substitution, pipelined evals with entry-grouped dH/dx terms, 5 waves/SIMD, time slicing "
+           "at step boundaries with least-attained-service issue priority)";
 }
 
 }  // extern "C"
