@@ -205,6 +205,30 @@ def test_time_slicing_concurrent_streams(problem, samples100, tracker):
         assert np.array_equal(h["tracks"].view(np.uint32), ref["tracks"].view(np.uint32))
 
 
+def test_time_slicing_falls_back_when_the_ring_does_not_fit(problem, samples100, tracker):
+    """A workspace sized for a smaller GPUHC_Max_Steps than the launch uses
+    (hc_trifocal_workspace_size_for_steps) cannot hold one ring entry per
+    possible suspension: the launch runs unsliced (ring counters untouched)
+    and still equals the serial run bit for bit."""
+    import torch
+    tgt, dif, _ = samples100
+    ref = tracker.track(tgt, dif).host()
+    dev = tracker.device
+    small = int(tracker.L.hc_trifocal_workspace_size_for_steps(tgt.shape[0], 10))
+    assert small < int(tracker.L.hc_trifocal_workspace_size_for_steps(tgt.shape[0], tracker.settings.max_steps))
+    ws = torch.zeros(small, dtype=torch.uint8, device=dev)
+    r = tracker.allocate(tgt.shape[0])
+    tracker.reset_tracks(r)
+    tracker.launch(torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev), r, workspace=ws)
+    torch.cuda.synchronize(dev)
+    off = int(tracker.L.hc_trifocal_workspace_size())
+    rq = np.frombuffer(ws[off:off + 768].cpu().numpy().tobytes(), np.uint32)
+    assert rq[64] == 0, "a launch whose ring does not fit must not slice"
+    h = r.host()
+    assert (h["converge"] == ref["converge"]).all()
+    assert np.array_equal(h["tracks"].view(np.uint32), ref["tracks"].view(np.uint32))
+
+
 def test_tracker_abort_mode(problem, samples100, tracker):
     """Config 3 semantics (abort on): the found hypothesis is one of the passing
     hypotheses of the abort-off run; tracked paths equal the abort-off results;
