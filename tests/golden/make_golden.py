@@ -117,9 +117,32 @@ def ph_codeopt_fixture(ss, sp, U, tgt, dif, explicit_rk=False):
     np.savez_compressed(os.path.join(HERE, name),
                         conv=conv, inf=inf, steps=st["steps"].astype(np.int16),
                         corrections=st["corrections"].astype(np.int16), hash=track_hash(tr),
-                        counts=np.array(O.count_solutions(tr, conv, inf)))
+                        counts=np.array(O.count_solutions(tr, conv, inf)), real=real_flags(tr, conv))
     print("PH" if explicit_rk else "PH_CodeOpt", "counts", O.count_solutions(tr, conv, inf), "stages",
           int(4 * st["steps"].sum() + st["corrections"].sum()))
+
+
+def real_flags(tracks, conv):
+    """Per path: converged and every |Im x_v| <= 1e-4 (Evaluations.cpp:145-182,
+    definitions.hpp:25) -- the 'real' column of *_Sols_Statistics per path."""
+    im_ok = (np.abs(tracks[:, :30, 1]).astype(np.float64) <= 1e-4).all(axis=1)
+    return (im_ok & (conv != 0)).astype(np.uint8)
+
+
+def add_real_flags(ss, sp, U, tgt, dif):
+    """Adds per-path `real` flags to gpuhc_N100_seed0.npz and
+    gpuhc_phcodeopt_N100_seed0.npz (fields kept; the re-run must reproduce the
+    committed hashes).  Input of the batch-id-prefix pin against the reference's
+    committed GPU_Sols_Statistics.txt (tests/test_oracle_kat.py)."""
+    for name, s in (("gpuhc_N100_seed0.npz", O.settings()),
+                    ("gpuhc_phcodeopt_N100_seed0.npz", O.settings(truncate=False))):
+        path = os.path.join(HERE, name)
+        old = dict(np.load(path))
+        tr, conv, inf, _ = O.gpuhc_track(ss, sp, tgt, dif, U, s)
+        assert np.array_equal(track_hash(tr), old["hash"]) and np.array_equal(conv, old["conv"]), name
+        old["real"] = real_flags(tr, conv)
+        np.savez_compressed(path, **old)
+        print(name, "real paths", int(old["real"].sum()), "converged", int(conv.sum()))
 
 
 def main():
@@ -129,6 +152,9 @@ def main():
     loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", "Triplet_Edgels_000.txt"))
     K = O.read_floats(os.path.join(RANS, "Intrinsic_Matrix.txt"), 9)
     tgt, dif, picked = O.prepare_target_params(0, [100], loc, tan, sp)
+    if only == "real":
+        add_real_flags(ss, sp, U, tgt, dif)
+        return
     if only in ("phcodeopt", "ph"):
         tgt, dif, _ = O.prepare_target_params(0, [100], loc, tan, sp)
         ph_codeopt_fixture(ss, sp, U, tgt, dif, explicit_rk=only == "ph")
@@ -154,7 +180,8 @@ def main():
                         conv=conv, inf=inf, steps=st["steps"].astype(np.int16),
                         corrections=st["corrections"].astype(np.int16), hash=track_hash(tr),
                         tracks_s01=tr[:624], counts=np.array(O.count_solutions(tr, conv, inf)),
-                        scored_ids=conv_ids.astype(np.int32), scored=scores.astype(np.int32))
+                        scored_ids=conv_ids.astype(np.int32), scored=scores.astype(np.int32),
+                        real=real_flags(tr, conv))
     print("gpuhc counts", O.count_solutions(tr, conv, inf), "passing", int(scores[:, 0].sum()))
 
     trc, cc, ic, stc, secs = O.cpuhc_track(ss, sp, tgt, dif, dhdx, dhdt)

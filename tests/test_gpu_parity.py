@@ -157,6 +157,12 @@ def test_tracker_matches_golden_N100(problem, samples100, tracker):
     assert (h == g["hash"]).all(), f"{(h != g['hash']).sum()} track hashes differ"
     from trifocal_pose_estimation_using_improved_gpuhc_amd import count_solutions
     assert tuple(g["counts"]) == count_solutions(r["tracks"], r["converge"], r["infinity"])
+    # per-path real flags: the input of the prefix pin against the reference's
+    # GPU_Sols_Statistics.txt (272 / 5; test_oracle_kat.py)
+    real = ((np.abs(r["tracks"][:, :30, 1]).astype(np.float64) <= 1e-4).all(axis=1) & (r["converge"] != 0))
+    assert np.array_equal(real.astype(np.uint8), g["real"])
+    cc, cr = np.cumsum(r["converge"].astype(np.int64)), np.cumsum(real.astype(np.int64))
+    assert (cc[2971:3006] == 272).all() and (cr[2971:3006] == 5).all()
 
 
 def test_time_slicing_is_bit_exact(problem, samples100, tracker):

@@ -187,6 +187,56 @@ def test_reference_output_files_parse():
     assert d["GPU_Timings_ms"] == [149.575]
 
 
+def _prefix_hits(d, conv_target, real_target):
+    """Batch-id prefix lengths n whose paths 0..n-1 hold exactly
+    (conv_target converged, real_target real) paths."""
+    cc = np.cumsum(d["conv"].astype(np.int64))
+    cr = np.cumsum(d["real"].astype(np.int64))
+    n = np.arange(1, len(cc) + 1)
+    return n[(cc == conv_target) & (cr == real_target)]
+
+
+def test_gpu_semantics_pinned_by_reference_gpu_statistics():
+    """The reference's committed GPU_Sols_Statistics.txt:1 (272 converged / 5
+    real / 495 'infinity') pins the GPU (TrunPaths) semantics -- depth-sign
+    pruning, the GPU LU's pivoting, the 32-slot norm tree -- which the CPU-HC
+    pin (KAT4) does not exercise.
+
+    That run is abort mode (..._TrunRANSAC.cu:45-327): a block reads the found
+    flag once when it starts (:148-152) and a block that started runs to
+    completion, so the tracked set is a batch-id prefix -- every path whose
+    block started before the first passing hypothesis raised the flag.  Its
+    counts are therefore the counts of a prefix of the full (abort-off) run,
+    which is the golden N=100 run (config 2's samples, srand(0)).  Asserted:
+      (a) some prefix n gives exactly (272, 5), and all such n form one window
+          (2972..3006 -- about 9.5 samples, one wave of resident 30-thread blocks);
+      (b) the first passing id (104, sample 0: the hypothesis that raised the
+          flag) lies before that window;
+      (c) the PH_CodeOpt semantics (no truncation, the archived kernel) reaches
+          272 converged only at a prefix whose real count is 8: no prefix gives
+          (272, 5), so the match discriminates the pruning semantics.
+    The third column (495) is the uninitialised 'infinity' flag of skipped
+    blocks and is not a property of the tracker.
+    Columns: GPU_HC_Solver.cpp:522-524 fills them swapped (reference_outputs.txt)."""
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    p = np.load(os.path.join(GOLDEN, "gpuhc_phcodeopt_N100_seed0.npz"))
+    assert int(g["real"].sum()) == int(g["counts"][1]) and int(p["real"].sum()) == int(p["counts"][1])
+    # the stored flags agree with the stored tracks of samples 0..1
+    im_ok = (np.abs(g["tracks_s01"][:, :30, 1]).astype(np.float64) <= 1e-4).all(axis=1)
+    assert np.array_equal(g["real"][:624], (im_ok & (g["conv"][:624] != 0)).astype(np.uint8))
+    hits = _prefix_hits(g, 272, 5)
+    assert len(hits) > 0
+    assert hits.max() - hits.min() + 1 == len(hits)          # one contiguous window
+    assert (hits.min(), hits.max()) == (2972, 3006), (hits.min(), hits.max())
+    passing = g["scored_ids"][g["scored"][:, 0] > 0]
+    assert passing.min() == 104 and passing.min() < hits.min()
+    assert len(_prefix_hits(p, 272, 5)) == 0
+    cc = np.cumsum(p["conv"].astype(np.int64))
+    cr = np.cumsum(p["real"].astype(np.int64))
+    at272 = np.nonzero(cc == 272)[0]
+    assert len(at272) > 0 and set(cr[at272].tolist()) == {8}
+
+
 def test_oracle_reproduces_golden_samples(problem, ransac0, oracle):
     g = np.load(os.path.join(GOLDEN, "samples_seed0.npz"))
     tgt, dif, picked = oracle.prepare_target_params(0, [100], ransac0.locations, ransac0.tangents,
