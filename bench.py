@@ -178,6 +178,7 @@ def main():
         tr.launch(tgt, dif, res, stream=stream)
         b_.record(stream)
     torch.cuda.synchronize(dev)
+    tr.workspace_status()   # raises on a device-side failure (table / time-slicing hand-over)
     launch_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
 
     # the papers' ablation ladder: the same launch through the archived
@@ -192,6 +193,7 @@ def main():
             tr.launch(tgt, dif, ab_buf, stream=stream, truncate=False, **kw)
             b_.record(stream)
         torch.cuda.synchronize(dev)
+        tr.workspace_status()
         h = ab_buf.host()
         return (float(np.median([a_.elapsed_time(b_) for a_, b_ in aev])),
                 int(4 * h["stats"]["steps"].astype(np.int64).sum() + h["stats"]["corrections"].astype(np.int64).sum()))

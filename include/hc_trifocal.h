@@ -164,9 +164,17 @@ hcStatus hc_trifocal_2op1p_30x30_track_ph_codeopt(const hcTrackArgs *args, void 
 hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspace,
                                           size_t workspace_bytes, hcStream stream);
 
-/* HC_SUCCESS, or HC_ERROR_TABLE when the last launch on this workspace found
-   an index table that does not fit the kernels' compaction (the tracker then
-   left every output untouched).  Blocking read -- call after synchronising. */
+/* Device-side outcome of the last launch on this workspace:
+     HC_SUCCESS;
+     HC_ERROR_TABLE  -- the index table does not fit the kernels' compaction
+                        (the tracker then left every output untouched);
+     HC_ERROR_DEVICE -- time slicing only: a suspended path could not be handed
+                        over (its ring entry never arrived within the bounded
+                        wait, or the ring overflowed); that path's converge /
+                        infinity / stats / track entry are not final.  The
+                        control block's ring_fail words hold the ticket, the tag
+                        seen, tail and head for diagnosis.
+   Blocking read -- call after synchronising. */
 hcStatus hc_trifocal_workspace_status(const void *workspace);
 
 /* Device timestamps of the last launch on this workspace, in seconds since the

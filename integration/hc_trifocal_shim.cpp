@@ -22,14 +22,18 @@
 //    concatenates them into the unified layout (Data_Reader.cpp:167-189) on the
 //    queue's stream before the launch.
 // The ABI never allocates on the hot path; the shim owns one workspace (and one
-// unified-table buffer for the Volta variants) per (device, stream), created on
-// first use and kept for the process lifetime.
+// unified-table buffer for the Volta variants) per (device, stream), allocated
+// by hc_trifocal_shim_reserve (hc_trifocal_shim.h, called from
+// GPU_HC_Solver::Allocate_Arrays) and kept for the process lifetime.  A launch
+// on a stream that was not reserved, or that needs more than was reserved,
+// grows the workspace on the hot path (synchronising the stream) and says so
+// once.
 #include <cstdio>
 #include <map>
 #include <mutex>
 #include <utility>
 
-#include "hc_trifocal.h"
+#include "hc_trifocal_shim.h"
 #include "magmaHC-kernels.hpp"
 
 namespace {
@@ -40,22 +44,19 @@ struct StreamState {
     void *workspace = nullptr;
     size_t ws_bytes = 0;
     int32_t *unified = nullptr;   // Volta variants only
+    int hot_grows = 0;            // launches that had to allocate
 };
 
-// the stream's workspace, grown to time-slicing size for launches of N samples
-// (hc_trifocal_workspace_size_for_steps; N = 0: abort mode, the base size)
-StreamState *state_for(hipStream_t s, bool need_unified, int N = 0, int max_steps = 80) {
-    static std::mutex mu;
-    static std::map<std::pair<int, hipStream_t>, StreamState> states;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-    std::lock_guard<std::mutex> g(mu);
-    StreamState &st = states[{dev, s}];
-    const size_t need = N > 0 ? hc_trifocal_workspace_size_for_steps(N, max_steps) : hc_trifocal_workspace_size();
+std::mutex g_mu;
+std::map<std::pair<int, hipStream_t>, StreamState> g_states;
+
+// (g_mu held) the stream's workspace grown to `need` bytes, the unified buffer if asked
+bool ensure(StreamState &st, hipStream_t s, size_t need, bool need_unified) {
     if (st.workspace && st.ws_bytes < need) {
         // the previous launch on this stream may still use it
-        if (hipStreamSynchronize(s) != hipSuccess || hipFree(st.workspace) != hipSuccess) return nullptr;
+        if (hipStreamSynchronize(s) != hipSuccess || hipFree(st.workspace) != hipSuccess) return false;
         st.workspace = nullptr;
+        st.ws_bytes = 0;
     }
     if (!st.workspace) {
         if (hipMalloc(&st.workspace, need) != hipSuccess) st.workspace = nullptr;
@@ -64,8 +65,22 @@ StreamState *state_for(hipStream_t s, bool need_unified, int N = 0, int max_step
     if (need_unified && !st.unified &&
         hipMalloc(reinterpret_cast<void **>(&st.unified), (kHxInts + kHtInts) * sizeof(int32_t)) != hipSuccess)
         st.unified = nullptr;
-    if (!st.workspace || (need_unified && !st.unified)) return nullptr;
-    return &st;
+    return st.workspace && (!need_unified || st.unified);
+}
+
+// the stream's state for a launch of N samples (N = 0: abort mode, the base
+// size); reserved streams return at once
+StreamState *state_for(hipStream_t s, bool need_unified, int N = 0, int max_steps = 80) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> g(g_mu);
+    StreamState &st = g_states[{dev, s}];
+    const size_t need = N > 0 ? hc_trifocal_workspace_size_for_steps(N, max_steps) : hc_trifocal_workspace_size();
+    if (st.workspace && st.ws_bytes >= need && (!need_unified || st.unified)) return &st;
+    if (st.hot_grows++ == 0)
+        printf("hc_trifocal_shim: allocating on the launch path (stream not reserved for %d samples at %d steps; "
+               "call hc_trifocal_shim_reserve from Allocate_Arrays)\n", N, max_steps);
+    return ensure(st, s, need, need_unified) ? &st : nullptr;
 }
 
 hcTrackArgs make_args(int sub_RANSAC_iters, int max_steps, int max_corr, int inc_steps,
@@ -142,6 +157,46 @@ real_Double_t track_abort(magma_queue_t q, int N, int E, int max_steps, int max_
 }
 
 }  // namespace
+
+extern "C" hcStatus hc_trifocal_shim_reserve(magma_queue_t queue, int max_samples, int max_steps) {
+    if (!queue || max_samples < 0 || max_steps < 0) return HC_ERROR_INVALID_VALUE;
+    const hipStream_t s = magma_queue_get_hip_stream(queue);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return HC_ERROR_DEVICE;
+    std::lock_guard<std::mutex> g(g_mu);
+    StreamState &st = g_states[{dev, s}];
+    const size_t need = max_samples > 0 ? hc_trifocal_workspace_size_for_steps(max_samples, max_steps)
+                                        : hc_trifocal_workspace_size();
+    if (!ensure(st, s, need, true)) return HC_ERROR_WORKSPACE;
+    return hipStreamSynchronize(s) == hipSuccess ? HC_SUCCESS : HC_ERROR_DEVICE;
+}
+
+extern "C" hcStatus hc_trifocal_shim_status(magma_queue_t queue) {
+    if (!queue) return HC_ERROR_INVALID_VALUE;
+    const hipStream_t s = magma_queue_get_hip_stream(queue);
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return HC_ERROR_DEVICE;
+    void *ws = nullptr;
+    {
+        std::lock_guard<std::mutex> g(g_mu);
+        auto it = g_states.find({dev, s});
+        if (it == g_states.end() || !it->second.workspace) return HC_SUCCESS;   // nothing launched here
+        ws = it->second.workspace;
+    }
+    if (hipStreamSynchronize(s) != hipSuccess) return HC_ERROR_DEVICE;
+    return hc_trifocal_workspace_status(ws);
+}
+
+extern "C" hcStatus hc_trifocal_shim_info(magma_queue_t queue, size_t *workspace_bytes, int *hot_path_grows) {
+    if (!queue || !workspace_bytes || !hot_path_grows) return HC_ERROR_INVALID_VALUE;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return HC_ERROR_DEVICE;
+    std::lock_guard<std::mutex> g(g_mu);
+    auto it = g_states.find({dev, magma_queue_get_hip_stream(queue)});
+    *workspace_bytes = it == g_states.end() ? 0 : it->second.ws_bytes;
+    *hot_path_grows = it == g_states.end() ? 0 : it->second.hot_grows;
+    return HC_SUCCESS;
+}
 
 real_Double_t kernel_GPUHC_trifocal_2op1p_30x30_PH_CodeOpt_TrunPaths(
     magma_queue_t my_queue, int sub_RANSAC_iters, int HC_max_steps, int HC_max_correction_steps,

@@ -55,6 +55,15 @@ def test_shim_exports_reference_signatures():
         assert name + sig in exported, f"{name}{sig} not exported"
 
 
+def test_shim_exports_reserve_and_status():
+    """The two calls GPU_HC_Solver adds (integration/hc_trifocal_shim.h): C linkage."""
+    assert os.path.exists(SHIM), "integration shim not built (__graft_entry__.build())"
+    out = subprocess.run(["nm", "-D", SHIM], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for name in ("hc_trifocal_shim_reserve", "hc_trifocal_shim_status", "hc_trifocal_shim_info"):
+        assert name in exported, name
+
+
 def _lib():
     from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
     _abi.lib()                      # the shim binds to the already loaded libhc_trifocal.so
@@ -62,6 +71,9 @@ def _lib():
     L.shim_queue_create.restype = C.c_void_p
     L.shim_queue_create.argtypes = [C.c_void_p]
     L.shim_queue_destroy.argtypes = [C.c_void_p]
+    L.hc_trifocal_shim_reserve.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    L.hc_trifocal_shim_status.argtypes = [C.c_void_p]
+    L.hc_trifocal_shim_info.argtypes = [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_int)]
     for f in ("shim_trunpaths", "shim_trunpaths_volta", "shim_trunransac", "shim_trunransac_volta",
               "shim_ph_codeopt", "shim_ph_codeopt_volta", "shim_ph"):
         getattr(L, f).restype = C.c_double
@@ -167,3 +179,55 @@ def test_shim_ph_launcher_matches_abi(problem, samples100, tracker):
     assert (conv.cpu().numpy().astype(np.uint8) == ref["converge"]).all()
     assert (inf.cpu().numpy().astype(np.uint8) == ref["infinity"]).all()
     assert np.array_equal(tracks.cpu().numpy()[:, :30], ref["tracks"][:, :30], equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_shim_reserved_stream_never_allocates(problem, samples100, tracker):
+    """hc_trifocal_shim_reserve (called from GPU_HC_Solver::Allocate_Arrays)
+    sizes the stream's workspace for time slicing up front: launches of up to
+    that many samples (plain and Volta) then never allocate on the launch path,
+    hc_trifocal_shim_status reports success after the launch, and the results
+    equal the ABI's.  A launch on a stream that was not reserved still works
+    (the lazy fallback) and is counted."""
+    import torch
+    L = _lib()
+    dev = tracker.device
+    N = 100
+    tgt, dif, _ = samples100
+    ref = tracker.track(tgt[:N], dif[:N]).host()
+    stream = torch.cuda.Stream(dev)
+    q = L.shim_queue_create(C.c_void_p(stream.cuda_stream))
+    s = tracker.settings
+    assert L.hc_trifocal_shim_reserve(C.c_void_p(q), N, s.max_steps) == 0
+    wsb, grows = C.c_size_t(0), C.c_int(-1)
+    assert L.hc_trifocal_shim_info(C.c_void_p(q), C.byref(wsb), C.byref(grows)) == 0
+    reserved = wsb.value
+    assert reserved == int(tracker.L.hc_trifocal_workspace_size_for_steps(N, s.max_steps)) and grows.value == 0
+    ss = torch.from_numpy(problem.start_sols).to(dev)
+    ssa = torch.tensor([ss.data_ptr() + k * 31 * 8 for k in range(312)], dtype=torch.int64, device=dev)
+    sp = torch.from_numpy(problem.start_params).to(dev)
+    tp = torch.from_numpy(np.ascontiguousarray(tgt[:N])).to(dev)
+    dp = torch.from_numpy(np.ascontiguousarray(dif[:N])).to(dev)
+    U = torch.from_numpy(problem.unified_index).to(dev)
+    hx = torch.from_numpy(np.ascontiguousarray(problem.dHdx_index.reshape(-1))).to(dev)
+    ht = torch.from_numpy(np.ascontiguousarray(problem.dHdt_index.reshape(-1))).to(dev)
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    torch.cuda.synchronize(dev)
+    for volta, n in ((False, N), (True, N), (False, 7)):
+        tracks = ss.unsqueeze(0).expand(n, -1, -1, -1).reshape(n * 312, 31, 2).contiguous()
+        tra = torch.tensor([tracks.data_ptr() + b * 31 * 8 for b in range(312 * n)], dtype=torch.int64, device=dev)
+        conv = torch.zeros(312 * n, dtype=torch.bool, device=dev)
+        inf = torch.zeros(312 * n, dtype=torch.bool, device=dev)
+        torch.cuda.synchronize(dev)
+        common = [C.c_int(s.max_steps), C.c_int(s.max_corrections), C.c_int(s.delta_t_inc_steps), p(ssa), p(tra),
+                  p(sp), p(tp), p(dp)]
+        if volta:
+            L.shim_trunpaths_volta(C.c_void_p(q), C.c_int(n), *common, p(hx), p(ht), p(conv), p(inf))
+        else:
+            L.shim_trunpaths(C.c_void_p(q), C.c_int(n), *common, p(U), p(conv), p(inf))
+        assert L.hc_trifocal_shim_status(C.c_void_p(q)) == 0
+        assert (conv.cpu().numpy().astype(np.uint8) == ref["converge"][:312 * n]).all()
+        assert np.array_equal(tracks.cpu().numpy()[:, :30], ref["tracks"][:312 * n, :30], equal_nan=True)
+    assert L.hc_trifocal_shim_info(C.c_void_p(q), C.byref(wsb), C.byref(grows)) == 0
+    assert grows.value == 0 and wsb.value == reserved
+    L.shim_queue_destroy(C.c_void_p(q))

@@ -126,7 +126,13 @@ class DeviceTracker:
         if workspace is None and not abort and time_slicing:
             need = int(self.L.hc_trifocal_workspace_size_for_steps(num_samples, self.settings.max_steps))
             if self.workspace.numel() < need:
+                # grown rarely (the first sliced launch of a size): the old
+                # workspace may still be in use by a launch on any stream, and
+                # the new one is zero-filled on the current stream, which need
+                # not be `stream` -- synchronise on both sides of the swap
+                torch.cuda.synchronize(self.device)
                 self.workspace = torch.zeros(need, dtype=torch.uint8, device=self.device)
+                torch.cuda.synchronize(self.device)
         ws_t = workspace if workspace is not None else self.workspace
         if ws_t.numel() < self.ws_bytes:
             raise _abi.HCError("workspace too small")
@@ -201,7 +207,11 @@ class DeviceTracker:
         return parts
 
     def workspace_status(self, workspace: torch.Tensor | None = None) -> None:
-        """Raises HCError if the last launch on workspace rejected the index table."""
+        """Raises HCError if the last launch on workspace failed on the device:
+        HC_ERROR_TABLE (the index table does not fit the compaction; outputs
+        untouched) or HC_ERROR_DEVICE (time slicing: a suspended path's ring
+        entry never came or the ring overflowed; the lost path's outputs are
+        not written; diagnostics in the control block's ring_fail words)."""
         ws = workspace if workspace is not None else self.workspace
         _abi.check(self.L.hc_trifocal_workspace_status(C.c_void_p(ws.data_ptr())), "hc_trifocal_workspace_status")
 
