@@ -1,6 +1,9 @@
 # usage: bash scripts/build_variant.sh NAME [extra hipcc flags...]
 # builds lib/libhc_trifocal_NAME.so: the product library with hc_kernels.hip
-# compiled with extra flags (A/B experiments, -DHC_DIAG_PHASES, -DHC_DIAG_TIMES)
+# compiled with extra flags: the diagnostic builds (-DHC_DIAG_PHASES,
+# -DHC_DIAG_TIMES [-DHC_DIAG_UTIL], -DHC_DIAG_LUWORK).  The round-2 A/B switches
+# (HC_LU_*, HC_EV_*, HC_HX_GROUPED, HC_AB_*, HC_CGESV4, HC_SLICE_Q, HC_PRIO_*)
+# were removed from the product sources in round 3; they live in commit 136b029.
 set -e
 cd "$(dirname "$0")/../trifocal_pose_estimation_using_improved_gpuhc_amd/csrc"
 N=$1; shift

@@ -3,9 +3,10 @@
 
     HC_TRIFOCAL_LIB=lib/libhc_trifocal_po.so python scripts/order_bound.py
 
-Needs the experiment build with -DHC_AB_PATH_ORDER (scripts/build_variant.sh po
--DHC_AB_PATH_ORDER), whose hc_ab_set_path_order sets an explicit per-path
-dequeue order.  Times config-2 launches (HIP events, median of 7) under:
+Needs the round-2 experiment build with -DHC_AB_PATH_ORDER, whose
+hc_ab_set_path_order sets an explicit per-path dequeue order.  That hook left
+the product tree in round 3; run this against the round-2
+sources: git worktree add /tmp/r2 136b029, then scripts/build_variant.sh there.  Times config-2 launches (HIP events, median of 7) under:
   builtin    the product's held-out per-track order
   lpt        the paths' ACTUAL costs from the golden run, longest first
              (clairvoyant; bounds every order)

@@ -15,7 +15,8 @@
 //    and use coef 0 with p[33] = x[30] = 1, so they add exact zeros to a +0
 //    accumulator (dH/dx) or to the finished sum (dH/dt, H; the reference also
 //    evaluates its padding terms);
-//  * the end-of-entry flag of a dH/dx term is the sign bit of its second word.
+//  * dH/dx terms are grouped by entry into slots of fixed capacity (below), so
+//    every entry ends at a compile-time term position on every lane.
 #pragma once
 
 #include <stddef.h>
@@ -26,10 +27,6 @@ namespace hc {
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
-#ifndef HC_HX_GROUPED
-#define HC_HX_GROUPED 1
-#endif
-#if HC_HX_GROUPED
 // dH/dx terms grouped by entry: a row's entries sorted by their number of
 // terms (largest first) go to entry slots 0..5, slot s holding at most
 // HX_GCAP[s] terms (this problem's maxima over the rows: 8, 5, 5, 5, 1, 1).
@@ -49,9 +46,6 @@ __host__ __device__ constexpr int hx_gslot(int k) {
     return k < hx_gend(0) ? 0 : k < hx_gend(1) ? 1 : k < hx_gend(2) ? 2 : k < hx_gend(3) ? 3 : k < hx_gend(4) ? 4 : 5;
 }
 static_assert(hx_gend(5) == HX_SLOT_CAP, "slot capacities");
-#else
-constexpr int HX_SLOT_CAP = 24;   // per-lane dH/dx terms (this problem: 23)
-#endif
 constexpr int SLOT_OFF_X = (int)offsetof(SlotLDS, x);
 constexpr int SLOT_OFF_P = (int)offsetof(SlotLDS, p);
 constexpr int SLOT_DIF_DELTA = (int)offsetof(SlotLDS, dif) - (int)offsetof(SlotLDS, p);
@@ -61,8 +55,8 @@ static_assert(SLOT_OFF_P + 8 * NPP < 65536, "p offsets must fit 16 bits");
 // Compacted tables, built once per launch by k_prep_tables from the
 // reference's padded unified index (Data_Reader.cpp:167-189).
 //  map[q][r]  (row r): column c -> entry slot (3 bits x 10 columns per word, 6 = structural zero)
-//  hx[k][r] (row r's k-th dH/dx term): .x = off(p[a]) | off(p[b]) << 16
-//                                      .y = off(x[u]) | off(x[v]) << 8 | (int8)coef << 16 | 8*slot << 24 | last << 31
+//  hx[k][r] (row r's k-th dH/dx term, entry slot hx_gslot(k)): .x = off(p[a]) | off(p[b]) << 16
+//                                      .y = off(x[u]) | off(x[v]) << 8 | (int8)coef << 16
 //  ht[j][r] (row r's j-th dH/dt / H term): .x = off(p[a]) | off(p[b]) << 16
 //                                      .y = off(x[u]) | off(x[v]) << 8 | off(x[w]) << 16 | (int8)coef << 24
 struct EvalTables {
@@ -108,16 +102,7 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
 // ahead of the previous terms' entry stores (which the compiler may not move
 // loads across), so a lane has several terms' LDS reads in flight instead of
 // one round trip per term, with few registers held.
-#ifndef HC_EV_AHEAD
-#define HC_EV_AHEAD 2
-#endif
-constexpr int EV_AHEAD = HC_EV_AHEAD;
-#ifndef HC_GATHER_BFE
-#define HC_GATHER_BFE 1
-#endif
-#ifndef HC_EV_SCHED
-#define HC_EV_SCHED 2
-#endif
+constexpr int EV_AHEAD = 2;
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
 struct HxOps { pf2 pa, pb, xu, xv; };
@@ -145,28 +130,19 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
         P = pcmul(P, q.pb);
         P = pcmul(P, q.xu);
         acc = pcmadd(acc, P, q.xv);
-#if HC_HX_GROUPED
         if (hx_is_gend(k)) {                 // static: the entry of slot hx_gslot(k) ends here on every lane
             if (r < NV) *reinterpret_cast<pf2 *>(eb + 8 * hx_gslot(k)) = acc;   // (padding lanes alias row 0)
             acc = pf2{0.0f, 0.0f};
         }
-#else
-        const bool last = (int)w[k].y < 0;   // last term of an entry (never set on padding terms)
-        *reinterpret_cast<pf2 *>(eb + (last ? ((w[k].y >> 24) & 0x7Fu) : 8u * 6u)) = acc;
-        acc = last ? pf2{0.0f, 0.0f} : acc;
-#endif
-#if HC_EV_SCHED >= 2
         __builtin_amdgcn_sched_barrier(0);
-#endif
     }
 }
 
 // dH/dx: row r of both paths' Jacobians into rA.  The term loop is fully
-// unrolled over the padded table (HX_SLOT_CAP words per lane; the caller stages
-// all of them) and branch-free, so the scheduler can keep several terms' LDS
-// reads in flight: every term stores its running sum -- to its entry slot when
-// it is the entry's last term, else to the lane's structural-zero slot 6 as a
-// scratch word -- and slot 6 is re-zeroed before the gather.
+// unrolled over the padded table (HX_SLOT_CAP words per lane) and branch-free,
+// so several terms' LDS reads stay in flight; each entry slot is stored once,
+// where its group of terms ends, slot 6 (structural zero) is zeroed, and 30
+// gathers through the column -> slot map rebuild the register row.
 __device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t (&map)[3], SlotLDS &S,
                                         int r) {
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
@@ -179,7 +155,6 @@ __device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const u
     // of the path loop (30 VGPRs held across the LU, then spilled)
     uint32_t m[3] = {map[0], map[1], map[2]};
     asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]));
-#if HC_GATHER_BFE
     // slot = v_bfe_u32, address = v_lshl_add_u32 (2 VALU per column, not 3)
     const char *eb = reinterpret_cast<const char *>(ent_row);
 #pragma unroll
@@ -188,13 +163,6 @@ __device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const u
         asm("v_bfe_u32 %0, %1, %2, 3" : "=v"(code) : "v"(m[c / 10]), "i"(3 * (c % 10)));
         rA[c] = *reinterpret_cast<const cf *>(eb + (code << 3));
     }
-#else
-#pragma unroll
-    for (int c = 0; c < NV; c++) {
-        const uint32_t code = (m[c / 10] >> (3 * (c % 10))) & 7u;
-        rA[c] = ent_row[code];
-    }
-#endif
 }
 
 struct HtOps { pf2 pa, pb, da, db, xu, xv, xw; };
@@ -224,9 +192,7 @@ __device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r
         s = s * pf2{co, co};
         const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
         acc = pcmsub(acc, P, q.xw);
-#if HC_EV_SCHED
         __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
-#endif
     }
     return cmk(acc.x, acc.y);
 }
@@ -256,9 +222,7 @@ __device__ __forceinline__ cf eval_h(const uint2 *s_ht, const SlotLDS &S, int r)
         pf2 P = q.pa * pf2{co, co};
         P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
         acc = pcmadd(acc, P, q.xw);
-#if HC_EV_SCHED
         __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     return cmk(acc.x, acc.y);
 }

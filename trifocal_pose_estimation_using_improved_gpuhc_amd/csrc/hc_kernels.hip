@@ -15,9 +15,6 @@
 // paths on the device and raises an agent-scope flag.
 #include "hc_device.hpp"
 #include "hc_lu.hpp"
-#ifdef HC_CGESV4
-#include "hc_lu4.hpp"
-#endif
 #include "../../include/hc_trifocal.h"
 
 #include <cstdlib>
@@ -38,21 +35,9 @@ static inline hcStatus launch_status(hcStatus on_fail) {
 // queue position q -> track c_track_order[q / N], sample q % N.  Results are
 // per batch id, so the order only changes when a path runs, not what it computes.
 __constant__ int c_track_order[NTRK] = {
-#ifdef HC_AB_TRACK_ORDER
-#include HC_AB_TRACK_ORDER
-#else
 #include "hc_track_order.inc"
-#endif
 };
-#ifdef HC_AB_PATH_ORDER
-// experiment build only: an explicit per-path dequeue order (device array set
-// by hc_ab_set_path_order), to bound what any dequeue order can gain
-__device__ const int *g_ab_path_order = nullptr;
-#endif
 __device__ __forceinline__ int path_of_queue_pos(int q, int num_paths, int ordered) {
-#ifdef HC_AB_PATH_ORDER
-    if (g_ab_path_order) return g_ab_path_order[q];
-#endif
     if (!ordered) return q;
     const int n = num_paths / NTRK;          // samples in this launch
     const int rank = q / n;
@@ -102,16 +87,7 @@ struct PathState {
     int stepidx, nsteps, ncorr, succ, flags, pad;
 };
 static_assert(sizeof(PathState) == 32, "PathState is 32 bytes");
-#ifndef HC_SLICE_Q
-#define HC_SLICE_Q 3
-#endif
-constexpr int SLICE_Q = HC_SLICE_Q;          // steps per time slice (0: no slicing)
-#ifndef HC_PRIO_LAS
-#define HC_PRIO_LAS 1
-#endif
-#ifndef HC_PRIO_ABORT
-#define HC_PRIO_ABORT 1
-#endif
+constexpr int SLICE_Q = 3;          // steps per time slice (profiles/r2n_ab_slice*.jsonl)
 // Ring: one entry per ticket, never reused within a launch.  A path is
 // suspended only after running SLICE_Q steps since it (re)started and runs at
 // most max_steps + 1 steps, so a launch pushes at most
@@ -270,7 +246,6 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
         bool bad = false;
         uint32_t map[3] = {0u, 0u, 0u};
         for (int c = 0; c < NV; c++) map[c / 10] |= 6u << (3 * (c % 10));
-#if HC_HX_GROUPED
         // entries sorted by their number of non-zero terms, largest first (ties:
         // lower column first); entry s fills slot s's HX_GCAP[s] term words,
         // padded with coefficient-0 terms
@@ -319,37 +294,7 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
                 slot++;
             }
         }
-#else
-        if (r < NV) {
-            for (int c = 0; c < NV; c++) {
-                int last_j = -1;
-                for (int j = 0; j < HX_TERMS; j++)
-                    if (U[(c * HX_TERMS + j) * HX_PARTS * NV + r] != 0) last_j = j;
-                if (last_j < 0) continue;
-                for (int j = 0; j <= last_j; j++) {
-                    const int base = (c * HX_TERMS + j) * HX_PARTS * NV + r;
-                    const int co = U[base], a = U[base + NV], b = U[base + 2 * NV], u = U[base + 3 * NV],
-                              v = U[base + 4 * NV];
-                    if (co == 0) continue;
-                    bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
-                           v < 0 || v > NV || slot >= 6;
-                    if (n < HX_SLOT_CAP && !bad)
-                        T->hx[n * 32 + r] = make_uint2(
-                            (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
-                            (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
-                                (((uint32_t)co & 0xFFu) << 16) | ((uint32_t)(8 * slot) << 24) |
-                                ((uint32_t)(j == last_j) << 31));
-                    n++;
-                }
-                if (slot < 6) map[c / 10] = (map[c / 10] & ~(7u << (3 * (c % 10)))) | ((uint32_t)slot << (3 * (c % 10)));
-                slot++;
-            }
-        }
-#endif
         if (n > HX_SLOT_CAP) bad = true;
-#if !HC_HX_GROUPED
-        for (int k2 = n; k2 < HX_SLOT_CAP; k2++) T->hx[k2 * 32 + r] = pad_hx;
-#endif
         for (int q = 0; q < 3; q++) T->map[q][r] = map[q];
         s_len[r] = n;
         const int32_t *D = U + HX_SIZE;
@@ -742,7 +687,6 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             }
         }
 #endif
-#if HC_PRIO_ABORT
         if (ABORT) {
             // Abort mode: first come, first served.  The queue is sample-major,
             // so the waves holding the earliest hypotheses get the higher issue
@@ -759,7 +703,6 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-#endif
         if (!ABORT && a.ordered && a.slice_q == 0) {
             // Without time slicing: issue priority by queue position (s_setprio,
             // arbitration among the waves of a SIMD): the last tenth of the
@@ -775,7 +718,6 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             else if (lvl >= PRIO_TENTHS - 3) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-#if HC_PRIO_LAS
         if (!ABORT && a.slice_q > 0) {
             // With time slicing: issue priority to the wave whose paths have
             // run the fewest steps (least attained service): a path's remaining
@@ -790,7 +732,6 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
             else __builtin_amdgcn_s_setprio(0);
         }
-#endif
         HC_DIAG_MARK(0);
         // the found flag for the next step boundary: read now, used after the stage
         if (ABORT && a.inflight_stop) found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -968,38 +909,6 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restric
     if (ok) X[(size_t)sys * NV + r] = x;
 }
 
-#ifdef HC_CGESV4
-// Experiment build only (-DHC_CGESV4, scripts/lu_ab.py): the LU
-// with four systems per wave (hc_lu4.hpp), lane q of group g holds rows q, q + 16.
-// Bit-identical, 27 % slower than k_cgesv (3 waves/SIMD instead of 5).
-__global__ void __launch_bounds__(WG_THREADS) k_cgesv4(int n, const cf *__restrict__ A, const cf *__restrict__ B,
-                                                       cf *__restrict__ X) {
-    __shared__ LUBuf4 s_lu[4 * WAVES_PER_WG];
-    const int lane = lane_id();
-    const int q = lane & 15, g = lane >> 4, w = threadIdx.x / WAVE;
-    const int sys0 = (blockIdx.x * WAVES_PER_WG + w) * 4;
-    const int sys = sys0 + g;
-    const bool ok = sys < n, r1ok = q < NV - 16;
-    cf a0[NV], a1[NV];
-    uint32_t p0 = 0, p1 = 0;
-#pragma unroll
-    for (int c = 0; c < NV; c++) {
-        a0[c] = ok ? A[((size_t)sys * NV + q) * NV + c] : cmk(0.0f, 0.0f);
-        a1[c] = (ok && r1ok) ? A[((size_t)sys * NV + q + 16) * NV + c] : cmk(0.0f, 0.0f);
-        if (a0[c].x != 0.0f || a0[c].y != 0.0f) p0 |= 1u << c;   // NaN counts as non-zero
-        if (a1[c].x != 0.0f || a1[c].y != 0.0f) p1 |= 1u << c;
-    }
-    const cf b0 = ok ? B[(size_t)sys * NV + q] : cmk(0.0f, 0.0f);
-    const cf b1 = (ok && r1ok) ? B[(size_t)sys * NV + q + 16] : cmk(0.0f, 0.0f);
-    unsigned act = 0u;
-#pragma unroll
-    for (int k = 0; k < 4; k++) act |= (sys0 + k < n) ? 1u << k : 0u;
-    cf x0, x1;
-    lu_solve4(a0, a1, b0, b1, lane, p0, p1, act, s_lu[w * 4 + g], x0, x1);
-    if (ok) X[(size_t)sys * NV + q] = x0;
-    if (ok && r1ok) X[(size_t)sys * NV + q + 16] = x1;
-}
-#endif
 
 // dH/dx, dH/dt, H at n points: one point per half-wave
 __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws, const cf *__restrict__ X,
@@ -1106,9 +1015,6 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.ordered = abort_mode ? 0 : 1;
     k.truncate = truncate ? 1 : 0;
     k.explicit_rk = explicit_rk ? 1 : 0;
-#ifdef HC_AB_NATURAL_ORDER
-    k.ordered = 0;
-#endif
     k.max_steps = t->settings.max_steps;
     k.max_corr = t->settings.max_corrections;
     k.inc_steps = t->settings.delta_t_inc_steps;
@@ -1264,15 +1170,9 @@ hcStatus hc_cgesv_30x30_batched(int n, const hcComplex *A, const hcComplex *b, h
     if (n < 0 || (n > 0 && (!A || !b || !x))) return HC_ERROR_INVALID_VALUE;
     if (n == 0) return HC_SUCCESS;
     (void)hipGetLastError();
-#ifdef HC_CGESV4
-    const int per = 4 * hc::WAVES_PER_WG;
-    hipLaunchKernelGGL(hc::k_cgesv4, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
-                       (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
-#else
     const int per = 2 * hc::WAVES_PER_WG;
     hipLaunchKernelGGL(hc::k_cgesv, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, (hipStream_t)stream, n,
                        (const hc::cf *)A, (const hc::cf *)b, (hc::cf *)x);
-#endif
     return hc::launch_status(HC_ERROR_LAUNCH);
 }
 
@@ -1316,13 +1216,6 @@ int hc_diag_util(unsigned long long *out, int reset) {
         if (hipGetSymbolAddress(&p, HIP_SYMBOL(hc::g_diag_util)) != hipSuccess || hipMemset(p, 0, n) != hipSuccess) return -1;
     }
     return 0;
-}
-#endif
-#ifdef HC_AB_PATH_ORDER
-// experiment build only: dequeue order = order[q] (a device array of the
-// launch's path ids, or null for the built-in order)
-int hc_ab_set_path_order(const int *order) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(hc::g_ab_path_order), &order, sizeof(order)) == hipSuccess ? 0 : -1;
 }
 #endif
 

@@ -60,19 +60,7 @@ struct alignas(16) LUBuf {
 static_assert(sizeof(LUBuf) <= sizeof(cf) * NV * 7, "LUBuf must fit in SlotLDS::ent");
 static_assert(offsetof(SlotLDS, ent) % 16 == 0, "SlotLDS::ent must be 16-B aligned");
 
-#ifndef HC_LU_CHUNK
-#define HC_LU_CHUNK 4
-#endif
-constexpr int LU_CHUNK = HC_LU_CHUNK;   // columns per skippable group (even)
-#ifndef HC_LU_SQCHECK
-#define HC_LU_SQCHECK 1
-#endif
-#ifndef HC_LU_PATBR
-#define HC_LU_PATBR 1
-#endif
-#ifndef HC_LU_BSEXEC
-#define HC_LU_BSEXEC 1
-#endif
+constexpr int LU_CHUNK = 4;   // columns per skippable group (even)
 
 // Correctly rounded 1/s for s in [2^-90, 2^120): v_rcp_f32 plus one Newton
 // step (bit-identical to hipcc's div_scale / div_fmas / div_fixup sequence
@@ -317,25 +305,17 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         // below whose column I may be non-zero takes the pivot patterns (both
         // halves': a superset of its own pivot row's); after a dense step
         // nothing is known zero.
-#if HC_LU_PATBR
         // dense step: every row below becomes dense (a uniform branch, taken
         // rarely; asm keeps it from being if-converted into a per-step select)
         if (__builtin_expect(dense, 0)) {
             if (below) asm volatile("v_mov_b32 %0, -1" : "=v"(pat));
         }
-#else
-        const uint32_t pmwd = dense ? 0xFFFFFFFFu : pmw;
-#endif
         if (below) {
             const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
-#if HC_LU_PATBR
             // v_bfe_i32 + v_and_or_b32 (after a dense step pat is all ones already)
             pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-#else
-            pat |= (((pat >> I) & 1u) != 0u || dense) ? pmwd : 0u;
-#endif
             lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, L
 #ifdef HC_DIAG_LUWORK
                             , lu_work_acc
@@ -365,7 +345,6 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
         const float y0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o0));
         const float x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.x), o1));
         const float y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o1));
-#if HC_LU_BSEXEC
         // x_I of each half from its SGPR pair: one v_mov_b64 for all lanes, one
         // more with the low half masked off (exec_lo saved and restored; the
         // tracker's solves run with full exec) -- instead of 4 v_mov + 2 v_cndmask
@@ -376,9 +355,6 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
                      "v_mov_b64 %0, %3\n\ts_mov_b32 exec_lo, %1"
                      : "=&v"(xv), "=&s"(tmp) : "s"(xs0), "s"(xs1));
         const cf xi = cmk(xv.x, xv.y);
-#else
-        const cf xi = hb ? cmk(x1, y1) : cmk(x0, y0);
-#endif
         if (rowid < I) {
             const pf2 w = pcmsub(pf2{rB.x, rB.y}, pf2{xi.x, xi.y}, pf2{rA[I].x, rA[I].y});
             rB = cmk(w.x, w.y);
@@ -394,7 +370,6 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L,
                                       unsigned long long count_mask = ~0ull) {
     (void)count_mask;   // diagnostic builds (HC_DIAG_LUWORK): lanes whose executed work is counted
-#if HC_LU_SQCHECK
     // every entry finite and below 2^64 in magnitude (inside the 2^88 the
     // sparse path needs): the per-component sums of squares (v_pk_fma_f32, 30
     // VALU) stay finite only then -- NaN propagates, an inf or |entry| >= 2^64
@@ -407,13 +382,6 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
         asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(sq) : "v"(e));
     }
     const bool ok = sq.x + sq.y < __builtin_inff();
-#else
-    // every entry finite and below 2^88 in magnitude (NaN fails the compare)
-    bool ok = true;
-#pragma unroll
-    for (int c = 0; c < NV; c++)
-        ok = ok && __builtin_fabsf(rA[c].x) < 0x1p88f && __builtin_fabsf(rA[c].y) < 0x1p88f;
-#endif
     const bool all_dense = __builtin_amdgcn_ballot_w64(!ok) != 0ull;   // then every step is dense
     const int r = lane & 31, hb = lane & 32;
     const bool row_lane = r < NV;
