@@ -153,14 +153,29 @@ struct LuChunks {
     static constexpr uint32_t mask(int I, int k) { return ((1u << len(I, k)) - 1u) << start(I, k); }
 };
 
+// Group tests on one bit: gbits = pmw | pmw >> 1 | pmw >> 2 | pmw >> 3, so bit J
+// says "some column of J..J+3 may be non-zero" and a group test is s_bitcmp1
+// + s_cbranch (the compiler keeps an s_cmp after a multi-bit s_and).
+__device__ __forceinline__ uint32_t group_bits(uint32_t pmw) {
+    const uint32_t t = pmw | (pmw >> 1);
+    return t | (t >> 2);
+}
+template <int I, int K>
+__device__ __forceinline__ bool group_live(uint32_t pmw, uint32_t gb) {
+    using C = LuChunks<LU_CHUNK>;
+    constexpr int J = C::start(I, K), N = C::len(I, K);
+    if constexpr (N == 1) return (pmw >> J) & 1u;
+    else return (gb >> J) & 1u;
+}
+
 // pivot lane: row elements of the groups of step I that are non-zero in some
 // pivot row of the wave
 template <int I, int K>
-__device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, LUBuf &L) {
+__device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uint32_t gb, LUBuf &L) {
     using C = LuChunks<LU_CHUNK>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (pmw & C::mask(I, K)) {
+        if (__builtin_expect(group_live<I, K>(pmw, gb), 1)) {
             if constexpr (N == 1) {
                 L.row[J] = rA[J];
             } else {
@@ -168,7 +183,7 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, LUB
                 for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
             }
         }
-        lu_put_row<I, K + 1>(rA, pmw, L);
+        lu_put_row<I, K + 1>(rA, pmw, gb, L);
     }
 }
 
@@ -179,22 +194,23 @@ __device__ unsigned long long g_diag_luwork[2];
 struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work counts (active path slots)
 #define HC_LU_WORK(ncols) (lu_work_acc.acc += (unsigned long long)(ncols) * \
     (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask))
+#define HC_LU_WORK_ARG , LuWork &lu_work_acc
+#define HC_LU_WORK_PASS , lu_work_acc
 #else
 #define HC_LU_WORK(ncols) do { } while (0)
+#define HC_LU_WORK_ARG
+#define HC_LU_WORK_PASS
 #endif
 
 // a_j -= l * u_j for the groups K.. of step I (the caller is inside the
 // below-the-pivot exec region)
 template <int I, int K>
-__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, const LUBuf &L
-#ifdef HC_DIAG_LUWORK
-                                          , LuWork &lu_work_acc
-#endif
-) {
+__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, uint32_t gb,
+                                          const LUBuf &L HC_LU_WORK_ARG) {
     using C = LuChunks<LU_CHUNK>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (pmw & C::mask(I, K)) {
+        if (__builtin_expect(group_live<I, K>(pmw, gb), 1)) {
             HC_LU_WORK(N);
             cf u[N];
             if constexpr (N == 1) {
@@ -210,21 +226,77 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        lu_update<I, K + 1>(rA, l, pmw, L
-#ifdef HC_DIAG_LUWORK
-                            , lu_work_acc
-#endif
-        );
+        lu_update<I, K + 1>(rA, l, pmw, gb, L HC_LU_WORK_PASS);
+    }
+}
+
+// The rest of pivot step I once the pivots are chosen: broadcast, relabel,
+// 1/pivot, update.  dense (a pivot outside the fast reciprocal range, or a
+// matrix not provably finite): every column group and the IEEE reciprocal.
+template <int I>
+__device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool dense, PivF &my,
+                                             LUBuf &L, bool is_piv, float piv_abs, int pl0, int pl1
+                                             HC_LU_WORK_ARG) {
+    // structural patterns of the two pivot rows (wave-uniform)
+    const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl0);
+    const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
+    constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
+    const uint32_t pmw = dense ? FULL : ((pp0 | pp1) & FULL);
+    const uint32_t gb = group_bits(pmw);
+    if (is_piv) {                                          // pivot row -> buffer
+        L.row[I] = rA[I];
+        lu_put_row<I, 0>(rA, pmw, gb, L);
+        L.row[30] = rB;
+        L.row[31].x = __int_as_float(rowid);
+    }
+    wave_lds_sync();
+    const cf sxi = L.row[I];
+    cf sB0, pr;
+    ld4(&L.row[30], sB0, pr);
+    const int piv_pos = __float_as_int(pr.x);
+    if (is_piv) rowid = I;                                 // :70-82
+    else if (rowid == I) rowid = piv_pos;
+    // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
+    cf reg;
+    divf f;
+    if (__builtin_expect(!dense, 1)) {
+        pf2 oo;
+        const pf2 rg = recip_fast(pf2{sxi.x, sxi.y}, piv_abs, oo);
+        reg = cmk(rg.x, rg.y);
+        f.o1 = oo.x;
+        f.o2 = oo.y;
+    } else {
+        f = cdiv_factors(sxi);
+        reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
+    }
+    if (is_piv) my.oo = pf2{f.o1, f.o2};
+    // opaque: the select chain must be resolved here, not carried as 30
+    // per-step factor pairs into the back substitution
+    asm volatile("" : "+v"(my.oo));
+    const bool below = rowid > I;                          // :86-93
+    // one exec-masked region per step: multiplier, right-hand side,
+    // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
+    // below whose column I may be non-zero takes the pivot patterns (both
+    // halves': a superset of its own pivot row's); after a dense step
+    // nothing is known zero.
+    // dense step: every row below becomes dense (a uniform branch, taken
+    // rarely; asm keeps it from being if-converted into a per-step select)
+    if (__builtin_expect(dense, 0)) {
+        if (below) asm volatile("v_mov_b32 %0, -1" : "=v"(pat));
+    }
+    if (below) {
+        const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+        const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
+        rB = cmk(bp.x, bp.y);
+        // v_bfe_i32 + v_and_or_b32 (after a dense step pat is all ones already)
+        pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
+        lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
     }
 }
 
 template <int I>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool all_dense, int lane,
-                                           int r, int hb, bool row_lane, PivF &my, LUBuf &L
-#ifdef HC_DIAG_LUWORK
-                                           , LuWork &lu_work_acc
-#endif
-) {
+                                           int r, int hb, bool row_lane, PivF &my, LUBuf &L HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
         const bool elig = rowid >= I && row_lane;
@@ -237,7 +309,10 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         const unsigned long long m = __builtin_amdgcn_ballot_w64(key == mx);
         const unsigned long long bad = __builtin_amdgcn_ballot_w64(!rcp_fast_bits(mx));
         const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
-        if (__builtin_expect(((mlo & (mlo - 1u)) | (mhi & (mhi - 1u))) != 0u || bad != 0ull || all_dense, 0)) {
+        // common: one maximum per half (two in the wave; s_bcnt1, where the
+        // per-half m & (m - 1) tests took six SALU), both in the fast range
+        const bool rare = (__builtin_popcountll(m) != 2) | (bad != 0ull) | all_dense;
+        if (__builtin_expect(rare, 0)) {
             // rare: NaN at position I wins (:57-64); exact ties: first position wins
             const bool isn = v != v;
             const int key2 = (elig && !isn) ? __float_as_int(v) : -1;
@@ -260,73 +335,12 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         } else {
             is_piv = key == mx;
             piv_abs = __int_as_float(mx);
-            pl0 = __builtin_ctz(mlo | 0x80000000u);
-            pl1 = 32 + __builtin_ctz(mhi | 0x80000000u);
+            pl0 = __builtin_ctz(mlo);        // exactly one bit per half here
+            pl1 = 32 + __builtin_ctz(mhi);
             dense = false;
         }
-        // structural patterns of the two pivot rows (wave-uniform)
-        const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl0);
-        const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
-        constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
-        const uint32_t pmw = dense ? FULL : ((pp0 | pp1) & FULL);
-        if (is_piv) {                                          // pivot row -> buffer
-            L.row[I] = rA[I];
-            lu_put_row<I, 0>(rA, pmw, L);
-            L.row[30] = rB;
-            L.row[31].x = __int_as_float(rowid);
-        }
-        wave_lds_sync();
-        const cf sxi = L.row[I];
-        cf sB0, pr;
-        ld4(&L.row[30], sB0, pr);
-        const int piv_pos = __float_as_int(pr.x);
-        if (is_piv) rowid = I;                                 // :70-82
-        else if (rowid == I) rowid = piv_pos;
-        // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
-        cf reg;
-        divf f;
-        if (__builtin_expect(!dense, 1)) {
-            pf2 oo;
-            const pf2 rg = recip_fast(pf2{sxi.x, sxi.y}, piv_abs, oo);
-            reg = cmk(rg.x, rg.y);
-            f.o1 = oo.x;
-            f.o2 = oo.y;
-        } else {
-            f = cdiv_factors(sxi);
-            reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
-        }
-        if (is_piv) my.oo = pf2{f.o1, f.o2};
-        // opaque: the select chain must be resolved here, not carried as 30
-        // per-step factor pairs into the back substitution
-        asm volatile("" : "+v"(my.oo));
-        const bool below = rowid > I;                          // :86-93
-        // one exec-masked region per step: multiplier, right-hand side,
-        // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
-        // below whose column I may be non-zero takes the pivot patterns (both
-        // halves': a superset of its own pivot row's); after a dense step
-        // nothing is known zero.
-        // dense step: every row below becomes dense (a uniform branch, taken
-        // rarely; asm keeps it from being if-converted into a per-step select)
-        if (__builtin_expect(dense, 0)) {
-            if (below) asm volatile("v_mov_b32 %0, -1" : "=v"(pat));
-        }
-        if (below) {
-            const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
-            const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
-            rB = cmk(bp.x, bp.y);
-            // v_bfe_i32 + v_and_or_b32 (after a dense step pat is all ones already)
-            pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-            lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, L
-#ifdef HC_DIAG_LUWORK
-                            , lu_work_acc
-#endif
-            );
-        }
-        lu_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L
-#ifdef HC_DIAG_LUWORK
-                          , lu_work_acc
-#endif
-        );
+        lu_step_body<I>(rA, rB, rowid, pat, dense, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
+        lu_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L HC_LU_WORK_PASS);
     }
 }
 
@@ -335,11 +349,11 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
 // lanes of its half with v_readlane (owner lane of each half found by a
 // ballot of the final row ids)
 template <int I>
-__device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, int hb) {
+__device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my) {
     if constexpr (I >= 0) {
         const unsigned long long own = __builtin_amdgcn_ballot_w64(rowid == I);
-        const int o0 = __builtin_ctz((unsigned)own | 0x80000000u);
-        const int o1 = 32 + __builtin_ctz((unsigned)(own >> 32) | 0x80000000u);
+        const int o0 = __builtin_ctz((unsigned)own);          // one owner per half
+        const int o1 = 32 + __builtin_ctz((unsigned)(own >> 32));
         const pf2 q = pcdiv_apply(pf2{rB.x, rB.y}, pf2{rA[I].x, rA[I].y}, my);
         const float x0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.x), o0));
         const float y0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o0));
@@ -360,7 +374,7 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
             rB = cmk(w.x, w.y);
         }
         if (rowid == I) rB = xi;   // the owner keeps its x_I (returned below)
-        lu_backward<I - 1>(rA, rB, rowid, my, hb);
+        lu_backward<I - 1>(rA, rB, rowid, my);
     }
 }
 
@@ -399,7 +413,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
 #else
     lu_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
 #endif
-    lu_backward<NV - 1>(rA, rB, rowid, my, hb);
+    lu_backward<NV - 1>(rA, rB, rowid, my);
     // lane r returns x_r: the owner of position r holds it in rB
     wave_lds_sync();
     if (row_lane) L.row[rowid] = rB;
