@@ -75,6 +75,8 @@ def parse():
                          "next batch's start); reported as config.pipelined_paths_per_s, 0 disables")
     ap.add_argument("--cpu-samples-4t", type=int, default=40,
                     help="samples of the 4-thread CPU-HC run (the reference's Num_Of_Cores default)")
+    ap.add_argument("--cpu-samples-ref", type=int, default=100,
+                    help="samples of the reference-build CPU-HC run (plain operators + OpenBLAS 0.3.23 cgesv)")
     return ap.parse_args()
 
 
@@ -247,15 +249,25 @@ def main():
         ra = tr.allocate(cnt, stats=True, abort=True)
         wss = []
         abort_info = {"samples_total": Sa * world, "samples_per_gpu": Sa, "chunk_samples": args.abort_chunk}
+        # the cross-process device flag (hcAbortArgs::peer_found): every GPU stops
+        # within a path of any GPU's find, not at its next chunk boundary
+        peer = sharding.SharedFlag(device=dev) if world > 1 else None
+        if peer is not None:
+            abort_info["cross_rank_stop"] = ("device flag over xGMI (hipIpc) + RCCL all_reduce at chunk boundaries"
+                                             if peer.ptr is not None else
+                                             f"RCCL all_reduce at chunk boundaries only ({peer.error})")
         for inflight in (False, True):
             ttfp, wall, tracked = [], [], []
             for _ in range(3):
                 tr.reset_tracks(ra)
                 torch.cuda.synchronize(dev)
-                if world > 1:
+                if peer is not None:
+                    peer.arm(stream)          # zeroed by its owner, then a barrier
+                elif world > 1:
                     dist.barrier()
                 w0 = time.perf_counter()
-                tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream, inflight_stop=inflight)
+                tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream, inflight_stop=inflight,
+                                        peer_found=peer if peer is not None and peer.ptr is not None else None)
                 torch.cuda.synchronize(dev)
                 w = time.perf_counter() - w0
                 hz = tr.read_timestamps(wss[0])[2]
@@ -280,6 +292,8 @@ def main():
                 "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3) if found else None,
                 "kernel_exit_wall_ms": round(float(np.median(wall)) * 1e3, 3),
                 "paths_tracked": int(np.median(tracked))}
+        if peer is not None:
+            peer.close()
         abort_info["note"] = ("device clock (s_memrealtime, rate from hipDeviceAttributeWallClockRate) from the "
                               "first chunk's start, min over ranks; wall = host time to the all-GPU sync, max "
                               "over ranks.  reference_semantics: paths in flight when the pose is found run to "
@@ -375,7 +389,8 @@ def main():
         if abort_info is not None:
             line["early_abort"] = abort_info
         if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(problem, data, args.cpu_samples, args.cpu_samples_4t, value)
+            line["cpu_baseline"] = cpu_baseline(problem, data, args.cpu_samples, args.cpu_samples_4t,
+                                                args.cpu_samples_ref, value)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -504,7 +519,7 @@ def reference_build_cpuhc(threads, n):
                     "reproduces Output_Write_Files/CPU_Sols_Statistics.txt exactly"}
 
 
-def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
+def cpu_baseline(problem, data, n_samples, n_samples_4t, n_samples_ref, gpu_value):
     """CPU baselines on this host's cores, bounded samples of the config-2 workload:
       value        the oracle's CPU-HC restatement (CPUHC_Generic_Solver_Eval_by_Indx
                    semantics: no path pruning, LAPACK-style cgesv, OpenMP dynamic
@@ -527,7 +542,7 @@ def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
         return 312 * n / secs, secs
     v, secs = run(n_samples, threads)
     v4, secs4 = run(n_samples_4t, 4)
-    ref = reference_build_cpuhc(threads, n_samples_4t)
+    ref = reference_build_cpuhc(threads, n_samples_ref)
     t0 = time.perf_counter()
     O.gpuhc_track(problem.start_sols, problem.start_params, tgt[:n_samples], dif[:n_samples], problem.unified_index,
                   O.settings(threads=threads))
@@ -539,7 +554,9 @@ def cpu_baseline(problem, data, n_samples, n_samples_4t, gpu_value):
                       f"wall on {threads} threads",
             "cpu_model": model, "host_logical_cpus": logical, "host_physical_cores": physical,
             "threads_note": "threads = this job's CPU share (OMP_NUM_THREADS; the GPU box allots 16 per GPU), "
-                            "capped by the physical cores",
+                            "capped by the physical cores.  No all-physical-cores leg: the box's 128 cores are "
+                            "shared with other jobs and this job may use 16 threads, so a 128-thread run would "
+                            "exceed its CPU share (the per-thread rate scales the 16-thread value)",
             "threads4": {"value": round(v4, 1), "cores": 4, "samples": n_samples_4t, "seconds": round(secs4, 2),
                          "note": "Num_Of_Cores default of gpuhc_settings.yaml:34"},
             "pruned_gpu_semantics": {"value": round(vp, 1), "cores": threads, "samples": n_samples,

@@ -109,6 +109,14 @@ typedef struct {
        like a skipped path (track untouched, converge = 0) -- a faster kernel
        exit, same time to the first good pose. */
     int inflight_stop;
+    /* Optional (NULL: none): a 4-byte flag shared by every process of a
+       multi-GPU run (hc_shared_flag_create on one rank, hc_shared_flag_open on
+       the others).  The launch sets it (system scope) when it finds a good
+       hypothesis and checks it, besides found_trifocal_sols, before it starts
+       each path -- and with inflight_stop at every step boundary -- so every GPU
+       stops within a path of any GPU's find instead of at its next launch.
+       The reference keeps one flag per GPU (GPU_HC_Solver.cpp:308-333). */
+    uint32_t *peer_found;
 } hcAbortArgs;
 
 /* Workspace: holds the compacted index tables, the path work queue and the
@@ -117,14 +125,19 @@ typedef struct {
 size_t hc_trifocal_workspace_size(void);
 
 /* Workspace size that also enables time slicing for launches of up to
-   sub_ransac_iters samples at GPUHC_Max_Steps = 80: 32 + 8 x 28 bytes per path
-   more (suspended paths' step-control state and the resume ring, one entry
-   per suspension).  With it, a path that has run a
+   sub_ransac_iters samples at GPUHC_Max_Steps = 80: 1 KB + (256 + 8 x 28)
+   bytes per path more (a suspended path's 256-byte state block and the resume
+   ring, one entry per suspension).  With it, a path that has run a
    slice of steps while other paths wait is suspended at a step boundary and
    resumed after the new paths (same results bit for bit; every path starts
    early, so a launch no longer ends with long paths that were dequeued late).
-   Tracking launches only (not abort mode).  A smaller workspace of at least
-   hc_trifocal_workspace_size() runs without slicing. */
+   Tracking launches only (not abort mode), and only while the step counters
+   fit the state block (GPUHC_Max_Steps < 16000, GPUHC_Max_Correction_Steps x
+   (GPUHC_Max_Steps + 2) < 65536, GPUHC_Num_Of_Steps_to_Increase_Delta_t <
+   16384).  A smaller workspace of at least hc_trifocal_workspace_size() runs
+   without slicing.  No initialisation is needed: the first launch on a
+   workspace builds its tables and clears its ring; later launches with the
+   same index table reuse the tables (an index-table hash is checked). */
 size_t hc_trifocal_workspace_size_for(int sub_ransac_iters);
 
 /* The same for a given GPUHC_Max_Steps (hc_trifocal_workspace_size_for assumes
@@ -142,6 +155,19 @@ hcStatus hc_trifocal_2op1p_30x30_track(const hcTrackArgs *args, void *workspace,
 hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAbortArgs *abort_args,
                                              void *workspace, size_t workspace_bytes,
                                              hcStream stream);
+
+/* The cross-process early-stop flag of hcAbortArgs::peer_found.  It lives in
+   the creating process's device memory (hipMalloc + hipIpcGetMemHandle); the
+   64-byte handle travels to the other processes (e.g. a torch.distributed
+   broadcast), which map it with hc_shared_flag_open (hipIpcOpenMemHandle, peer
+   access over xGMI).  create zeroes it; reset zeroes it on a stream before a
+   new run (the caller orders the reset before any rank's launch);
+   close(flag, opened = 1 for a handle opened here, 0 for the creator's). */
+typedef struct { unsigned char reserved[64]; } hcIpcHandle;   /* == hipIpcMemHandle_t */
+hcStatus hc_shared_flag_create(uint32_t **flag, hcIpcHandle *handle);
+hcStatus hc_shared_flag_open(const hcIpcHandle *handle, uint32_t **flag);
+hcStatus hc_shared_flag_reset(uint32_t *flag, hcStream stream);
+hcStatus hc_shared_flag_close(uint32_t *flag, int opened);
 
 /* GPU-HC tracking WITHOUT the depth-sign path truncation: every path runs
    until it converges, diverges or reaches the step limit.  Replaces the

@@ -69,16 +69,17 @@ def test_workspace_size_and_version():
 
 def test_workspace_size_for_time_slicing():
     """hc_trifocal_workspace_size_for(N): the base workspace + the time-slicing
-    area: ring counters, a 32-B PathState per path and an 8-B ring entry per
-    possible suspension -- at most (max_steps + 1) / 3 per path, never reused
-    within a launch (+1 per path, +64).  The plain form assumes max_steps = 80."""
+    area: ring counters (1 KB), a 256-B suspend block per path and an 8-B ring
+    entry per possible suspension -- at most (max_steps + 1) / 3 per path,
+    never reused within a launch (+1 per path, +64).  The plain form assumes
+    max_steps = 80."""
     from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
     L = _abi.lib()
     base = int(L.hc_trifocal_workspace_size())
     s0, s1, s100 = (int(L.hc_trifocal_workspace_size_for(n)) for n in (0, 1, 100))
     assert base < s0 <= s1 < s100
     assert s100 % 256 == 0
-    per_path = 32 + 8 * (81 // 3 + 1)
+    per_path = 256 + 8 * (81 // 3 + 1)
     assert per_path * 312 * 100 <= s100 - base <= per_path * 312 * 100 + 4096
     assert int(L.hc_trifocal_workspace_size_for(-5)) == s0
     assert int(L.hc_trifocal_workspace_size_for_steps(100, 80)) == s100

@@ -119,6 +119,82 @@ def test_two_ranks_share_cuda0_abort_and_pose(tmp_path, oracle, ransac0):
         assert x["merged"].tolist() == exp
 
 
+def _rank_main_shared_flag(rank, world, port, out_dir):
+    """One abort launch per rank over its whole shard (no chunk boundary to
+    carry the flag), in-flight stop on, with the cross-process SharedFlag."""
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from trifocal_pose_estimation_using_improved_gpuhc_amd import (load_problem, load_ransac_data,
+                                                                       prepare_target_params, sharding)
+        from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker
+        dev = torch.device("cuda:0")
+        problem = load_problem()
+        data = load_ransac_data(0)
+        tgt, dif, _ = prepare_target_params(problem, data, seed=0, num_samples=FIRST + TOTAL)
+        off, cnt = sharding.shard(TOTAL, world, rank)
+        t = torch.from_numpy(tgt[FIRST + off:FIRST + off + cnt]).to(dev)
+        d = torch.from_numpy(dif[FIRST + off:FIRST + off + cnt]).to(dev)
+        tr = DeviceTracker(problem, dev)
+        tr.set_ransac_data(data)
+        r = tr.allocate(cnt, stats=True, abort=True)
+        tr.reset_tracks(r)
+        flag = sharding.SharedFlag(device=dev)
+        assert flag.ptr is not None, flag.error
+        stream = torch.cuda.Stream(dev)
+        flag.arm(stream)
+        wss = []
+        parts = tr.launch_abort_chunked(t, d, r, cnt, wss, stream=stream, inflight_stop=True, peer_found=flag)
+        torch.cuda.synchronize(dev)
+        h = r.host()
+        dist.barrier()
+        flag.close()
+        np.savez(os.path.join(out_dir, f"rank{rank}.npz"), off=off, cnt=cnt, nchunks=len(parts),
+                 tracks=h["tracks"], conv=h["converge"], steps=h["stats"]["steps"],
+                 batch_index=h["batch_index"], found=h["found"])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_two_ranks_shared_flag_stops_other_rank_mid_launch(tmp_path, oracle, ransac0):
+    """The cross-process flag (hcAbortArgs::peer_found, sharding.SharedFlag) on
+    two ranks sharing cuda:0, each tracking its whole 49/50-sample shard in ONE
+    abort launch: rank 1's first hypothesis (sample 51) passes, and rank 0 --
+    which has no passing hypothesis and no chunk boundary to learn of it --
+    stops within that launch (fewer than its 15 600 paths completed).  Every
+    completed path equals the single-rank golden run, and the merged pose
+    equals the oracle's selection over both ranks' paths."""
+    import torch.multiprocessing as mp
+    sys.path.insert(0, GOLDEN)
+    from make_golden import track_hash
+    mp.start_processes(_rank_main_shared_flag, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True,
+                       start_method="spawn")
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    passing = set(int(b) for b, s in zip(g["scored_ids"], g["scored"]) if s[0] == 1)
+    R = [np.load(os.path.join(tmp_path, f"rank{r}.npz")) for r in range(2)]
+    assert [int(x["nchunks"]) for x in R] == [1, 1]
+    for x in R:
+        base = (FIRST + int(x["off"])) * 312
+        gl = slice(base, base + int(x["cnt"]) * 312)
+        done = x["steps"] > 0
+        assert (x["conv"][done] == g["conv"][gl][done]).all()
+        assert (track_hash(x["tracks"])[done] == g["hash"][gl][done]).all()
+        assert (x["conv"][~done] == 0).all()
+        ids = np.nonzero(x["batch_index"] >= 0)[0]
+        assert set(int(b) + base for b in ids) <= passing
+    r0, r1 = R
+    assert len(np.nonzero(r1["batch_index"] >= 0)[0]) > 0 and bool(r1["found"])
+    assert len(np.nonzero(r0["batch_index"] >= 0)[0]) == 0
+    assert bool(r0["found"])          # the chunk-boundary reduction still delivers the byte
+    n0 = int((r0["steps"] > 0).sum())
+    assert n0 < int(r0["cnt"]) * 312, f"rank 0 completed all {n0} paths: the peer flag never stopped it"
+
+
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("gpus", [2, 3])
 def test_cli_logical_gpus_share_device(tmp_path, gpus):
@@ -136,3 +212,23 @@ def test_cli_logical_gpus_share_device(tmp_path, gpus):
     gp = np.load(os.path.join(GOLDEN, "pose_N100_seed0.npz"))
     assert int(pr[0]) == 1 and [int(pr[5]), int(pr[6])] == gp["path"].tolist()
     assert int(pr[7]) == int(gp["num_candidates"])
+
+
+@pytest.mark.timeout(300)
+def test_cli_abort_across_gpus_share_device(tmp_path):
+    """magmaHC-main --abort --abort-across-gpus on 2 logical GPUs sharing device 0:
+    the C++ GPU_HC_Solver allocates one found flag for both launches
+    (Abort_Across_GPUs, hcAbortArgs::peer_found).  The run finds a pose that
+    matches GT, and it tracks no more than the abort-off golden run converges
+    (the skipped paths report conv = 0)."""
+    cli = os.path.join(ROOT, "trifocal_pose_estimation_using_improved_gpuhc_amd", "bin", "magmaHC-main")
+    shutil.copytree(os.path.join(ROOT, "data"), os.path.join(tmp_path, "data"))
+    out = subprocess.run([cli, "-p", "trifocal_2op1p_30x30", "-d", str(tmp_path), "-g", "2", "--share-devices",
+                          "--abort", "--inflight-stop", "--abort-across-gpus"],
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stdout + out.stderr
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    stats = [int(v) for v in open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Sols_Statistics.txt")).read().split()[:2]]
+    assert 0 < stats[0] <= int(g["counts"][0]) and stats[1] <= int(g["counts"][1])
+    pr = open(os.path.join(tmp_path, "Output_Write_Files", "GPU_Pose_Results.txt")).read().split()
+    assert int(pr[0]) == 1

@@ -64,7 +64,12 @@ class hcAbortArgs(C.Structure):
                 ("intrinsic_matrix", C.c_void_p),
                 ("found_trifocal_sols", C.c_void_p),
                 ("trifocal_sols_batch_index", C.c_void_p),
-                ("inflight_stop", C.c_int)]
+                ("inflight_stop", C.c_int),
+                ("peer_found", C.c_void_p)]
+
+
+class hcIpcHandle(C.Structure):
+    _fields_ = [("reserved", C.c_ubyte * 64)]
 
 
 _lib = None
@@ -125,6 +130,15 @@ def lib() -> C.CDLL:
         for fn in ("hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
                    "hc_count_triplet_edgels", "hc_read_triplet_edgels"):
             getattr(L, fn).restype = C.c_int
+        # (bound only where present: A/B runs load earlier builds through HC_TRIFOCAL_LIB;
+        # the product library exports them, tests/test_abi_host.py)
+        if hasattr(L, "hc_shared_flag_create"):
+            for fn in ("hc_shared_flag_create", "hc_shared_flag_open", "hc_shared_flag_reset", "hc_shared_flag_close"):
+                getattr(L, fn).restype = C.c_int
+            L.hc_shared_flag_create.argtypes = [C.POINTER(C.c_void_p), C.POINTER(hcIpcHandle)]
+            L.hc_shared_flag_open.argtypes = [C.POINTER(hcIpcHandle), C.POINTER(C.c_void_p)]
+            L.hc_shared_flag_reset.argtypes = [C.c_void_p, C.c_void_p]
+            L.hc_shared_flag_close.argtypes = [C.c_void_p, C.c_int]
         _lib = L
     return _lib
 
@@ -141,6 +155,7 @@ DECLARED_SYMBOLS = (
     "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
     "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
     "hc_last_error_string",
+    "hc_shared_flag_create", "hc_shared_flag_open", "hc_shared_flag_reset", "hc_shared_flag_close",
     "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
     "hc_count_triplet_edgels", "hc_read_triplet_edgels", "hc_split_samples", "hc_prepare_target_params",
     "hc_count_solutions",

@@ -115,6 +115,7 @@ GPU_HC_Solver::GPU_HC_Solver(const HC_Settings &S, const std::string &root_dir) 
     Num_Of_Tracks = S.i("Num_Of_Tracks", 312);
     Abort_RANSAC_by_Good_Sol = S.b("Abort_RANSAC_by_Good_Sol", false);
     Abort_Inflight_Stop = S.b("Abort_Inflight_Stop", false);
+    Abort_Across_GPUs = S.b("Abort_Across_GPUs", false);
     RANSAC_Dataset_Name = S.has("RANSAC_Dataset") ? S.str("RANSAC_Dataset") : "Synthetic";
     Num_Of_GPUs = S.i("Num_Of_GPUs", 1);
     Num_Of_RANSAC_Iterations = S.i("Num_Of_RANSAC_Iterations", 100);
@@ -256,6 +257,23 @@ void GPU_HC_Solver::Set_RANSAC_Abort_Arrays() {
         p->h_batch_index.assign(n, -1);
         p->h_found = 0;
     }
+    // Abort_Across_GPUs (not in the reference, which keeps one flag per GPU,
+    // GPU_HC_Solver.cpp:308-333): a 4-byte flag on the first GPU's device that
+    // every GPU's launch sets on a find and polls before each path
+    // (hcAbortArgs::peer_found, system-scope atomics over xGMI)
+    if (Abort_Across_GPUs && !gpus_.empty() && !d_peer_found) {
+        const int dev0 = gpus_[0]->dev;
+        for (PerGPU *p : gpus_) {
+            if (p->dev == dev0) continue;
+            HC_HIP_CHECK(hipSetDevice(p->dev));
+            const hipError_t e = hipDeviceEnablePeerAccess(dev0, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) HC_HIP_CHECK(e);
+            (void)hipGetLastError();
+        }
+        HC_HIP_CHECK(hipSetDevice(dev0));
+        HC_HIP_CHECK(hipMalloc(&d_peer_found, 256));
+        HC_HIP_CHECK(hipMemset(d_peer_found, 0, 256));
+    }
 }
 
 void GPU_HC_Solver::Data_Transfer_From_Host_To_Device() {
@@ -299,6 +317,8 @@ void GPU_HC_Solver::Data_Transfer_From_Host_To_Device() {
             HC_HIP_CHECK(hipMemcpyAsync(p->d_batch_index, p->h_batch_index.data(),
                                         p->h_batch_index.size() * sizeof(int32_t), hipMemcpyHostToDevice, p->stream));
             HC_HIP_CHECK(hipMemsetAsync(p->d_found, 0, 1, p->stream));
+            if (d_peer_found && p == gpus_.front())
+                HC_HIP_CHECK(hipMemsetAsync(d_peer_found, 0, sizeof(uint32_t), p->stream));
         }
         HC_HIP_CHECK(hipStreamSynchronize(p->stream));
         transfer_h2d_time[p->g] = now_s() - t0;
@@ -343,6 +363,7 @@ void GPU_HC_Solver::Solve_by_GPU_HC() {
             ab.found_trifocal_sols = p->d_found;
             ab.trifocal_sols_batch_index = p->d_batch_index;
             ab.inflight_stop = Abort_Inflight_Stop ? 1 : 0;
+            ab.peer_found = d_peer_found;
             st = hc_trifocal_2op1p_30x30_track_abort(&a, &ab, p->d_ws, p->ws_bytes, (hcStream)p->stream);
         } else {
             st = hc_trifocal_2op1p_30x30_track(&a, p->d_ws, p->ws_bytes, (hcStream)p->stream);
@@ -507,6 +528,10 @@ void GPU_HC_Solver::Free_Arrays_for_Aborting_RANSAC() {
         (void)hipFree(p->d_found);
         (void)hipFree(p->d_batch_index);
         p->d_found = nullptr;
+        if (d_peer_found && p == gpus_.front()) {
+            (void)hipFree(d_peer_found);
+            d_peer_found = nullptr;
+        }
         p->d_batch_index = nullptr;
     }
 }

@@ -62,7 +62,10 @@ static_assert(SLOT_OFF_P + 8 * NPP < 65536, "p offsets must fit 16 bits");
 struct EvalTables {
     int hx_len;
     int status;
-    int pad[2];
+    unsigned magic;                   // TAB_MAGIC once built: the tables persist in the workspace
+    unsigned pad;
+    unsigned long long src_hash;      // hash of the unified index they were built from
+    unsigned long long pad2;
     uint32_t map[3][32];
     uint2 hx[HX_SLOT_CAP * 32];
     uint2 ht[HT_TERMS * 32];
@@ -102,6 +105,9 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
 // ahead of the previous terms' entry stores (which the compiler may not move
 // loads across), so a lane has several terms' LDS reads in flight instead of
 // one round trip per term, with few registers held.
+#ifndef HC_X_EPAIR
+#define HC_X_EPAIR 0
+#endif
 constexpr int EV_AHEAD = 2;
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
@@ -134,7 +140,7 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
             if (r < NV) *reinterpret_cast<pf2 *>(eb + 8 * hx_gslot(k)) = acc;   // (padding lanes alias row 0)
             acc = pf2{0.0f, 0.0f};
         }
-        __builtin_amdgcn_sched_barrier(0);
+        if (!HC_X_EPAIR || (k & 1)) __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -192,7 +198,7 @@ __device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r
         s = s * pf2{co, co};
         const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
         acc = pcmsub(acc, P, q.xw);
-        __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
+        if (!HC_X_EPAIR || (j & 1)) __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
     }
     return cmk(acc.x, acc.y);
 }
@@ -222,7 +228,7 @@ __device__ __forceinline__ cf eval_h(const uint2 *s_ht, const SlotLDS &S, int r)
         pf2 P = q.pa * pf2{co, co};
         P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
         acc = pcmadd(acc, P, q.xw);
-        __builtin_amdgcn_sched_barrier(0);
+        if (!HC_X_EPAIR || (j & 1)) __builtin_amdgcn_sched_barrier(0);
     }
     return cmk(acc.x, acc.y);
 }

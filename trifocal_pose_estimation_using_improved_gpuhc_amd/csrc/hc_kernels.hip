@@ -18,6 +18,7 @@
 #include "../../include/hc_trifocal.h"
 
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 #include <utility>
@@ -50,7 +51,7 @@ constexpr int WAVES_PER_WG = WG_THREADS / WAVE;
 
 // The caller-owned workspace (hc_trifocal_workspace_size()).
 struct Workspace {
-    // control block, zeroed by the launcher every call (first 64 bytes)
+    // control block, zeroed by k_prep_tables every launch (first 64 bytes)
     unsigned queue;          // path work queue
     unsigned status;         // HC_ERROR_TABLE if the index table does not fit the compaction
     unsigned found;          // device-side "good hypothesis found" flag
@@ -65,15 +66,15 @@ struct Workspace {
 static_assert(offsetof(Workspace, tab) == 64, "control block is 64 bytes");
 
 // Time slicing.  A path that has run slice_q steps while other
-// work waits is suspended at its step boundary: x goes to its own track entry,
-// the step-control scalars to PathState, the path id to a FIFO ring.  While
-// new paths remain, the suspending half takes one (an unpaired push); after
-// that it swaps with the oldest suspended path (a paired push + pop, i.e.
-// round robin).  A half whose path ends takes a new path, else the oldest
-// suspended one.  Every path thus starts early and the end of a launch is
-// made of short remainders instead of whole late-dequeued long paths.
-// Bit-exact: at a step boundary x == x_last == the RK accumulator, and this
-// is the whole vector state.
+// work waits is suspended at its step boundary: x and its step-control scalars
+// go to the path's 256-B suspend block (two full cache lines, one store per
+// half), the path id to a FIFO ring.  While new paths remain, the suspending
+// half takes one (an unpaired push); after that it swaps with the oldest
+// suspended path (a paired push + pop, i.e. round robin).  A half whose path
+// ends takes a new path, else the oldest suspended one.  Every path thus starts
+// early and the end of a launch is made of short remainders instead of whole
+// late-dequeued long paths.  Bit-exact: at a step boundary x == x_last == the
+// RK accumulator, and this is the whole vector state.
 //
 // Ring protocol (no CAS loops): tickets from atomicAdd on head / tail; avail
 // counts published entries not yet claimed by unpaired pops (a semaphore:
@@ -81,13 +82,25 @@ static_assert(offsetof(Workspace, tab) == 64, "control block is 64 bytes");
 // positive, so concurrent failures cannot hide an entry).  A paired pop needs
 // no claim: its own push precedes it.  A claimed entry may still be in the
 // pusher's hands (ticket taken, entry not yet written), hence the short wait
-// on its sequence tag.
-struct PathState {
-    float t0, dt;
-    int stepidx, nsteps, ncorr, succ, flags, pad;
-};
-static_assert(sizeof(PathState) == 32, "PathState is 32 bytes");
-constexpr int SLICE_Q = 3;          // steps per time slice (profiles/r2n_ab_slice*.jsonl)
+// on its tag.  An entry's tag hashes the launch epoch with its ticket, so the
+// ring needs no clearing between launches (only once, when a workspace is
+// first used or its ring grows: k_prep_tables).
+//
+// Suspend block of path b (32 x 8 B): words 0..29 = x, word 30 = (t0, dt),
+// word 31 = (stepidx | nsteps << 16, ncorr | succ << 16 | flags << 30); the
+// launcher enables slicing only where these fields fit (slice_fits).
+constexpr int SUSP_WORDS = 32;
+#ifndef HC_X_MINW
+#define HC_X_MINW 5
+#endif
+#ifndef HC_X_SLICE_Q
+#define HC_X_SLICE_Q 3
+#endif
+constexpr int SLICE_Q = HC_X_SLICE_Q;          // steps per time slice (profiles/r2n_ab_slice*.jsonl)
+__host__ __device__ constexpr bool slice_fits(int max_steps, int max_corr, int inc_steps) {
+    return max_steps >= 0 && max_steps < 16000 && inc_steps >= 0 && inc_steps < 16384 && max_corr >= 0 &&
+           (long long)max_corr * (max_steps + 2) < 65536;
+}
 // Ring: one entry per ticket, never reused within a launch.  A path is
 // suspended only after running SLICE_Q steps since it (re)started and runs at
 // most max_steps + 1 steps, so a launch pushes at most
@@ -126,24 +139,41 @@ struct KArgs {
     const float *edgels;
     const float *K;
     uint8_t *found_flag;
+    unsigned *peer_found;           // cross-process flag of a multi-GPU run (hcAbortArgs::peer_found), or null
     int32_t *batch_index;
     // time slicing (slice_q > 0; tracking without abort only)
     int slice_q;
     unsigned ring_cap;
-    unsigned *rq;                   // ring counters, one 256-B line each: [0] head, [64] tail, [128] avail
-    PathState *pst;                 // per path id
-    unsigned long long *ring;       // (ticket + 1) << 32 | path id
+    unsigned *rq;                   // ring counters, one 256-B line each: [0] head, [64] tail, [128] avail, [192] meta
+    unsigned long long *susp;       // suspend blocks, SUSP_WORDS per path id
+    unsigned long long *ring;       // ring_tag(epoch, ticket) << 32 | path id
 };
-constexpr int RQ_HEAD = 0, RQ_TAIL = 64, RQ_AVAIL = 128, RQ_WORDS = 192;
+// rq layout: counters zeroed by k_prep_tables every launch; meta: the launch
+// epoch, a magic word and the ring entries already cleared (persist)
+constexpr int RQ_HEAD = 0, RQ_TAIL = 64, RQ_AVAIL = 128, RQ_EPOCH = 192, RQ_MAGIC = 193, RQ_CLEARED = 194,
+              RQ_WORDS = 256;
+constexpr unsigned RQ_MAGIC_VALUE = 0x48435452u;   // "HCTR"
+// tag of ticket t's entry in launch `epoch` (never 0, so a cleared entry never
+// matches; distinct epochs give distinct tags for the same ticket)
+__device__ __forceinline__ unsigned ring_tag(unsigned epoch, unsigned t) {
+    return ((epoch * 0x9E3779B1u) ^ (t * 0x85EBCA6Bu)) | 1u;
+}
 
 __device__ __forceinline__ unsigned ld_rlx(const unsigned *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// The hand-over data of a suspended path (x, PathState, ring entries) is
-// written and read with agent-scope relaxed atomics (coherent across the
-// XCDs' L2s without cache-wide fences); the writer drains its stores
-// (s_waitcnt vmcnt(0)) before publishing the ring entry, and the reader's
-// loads depend on the entry's path id.
+// The hand-over data of a suspended path (suspend block, ring entries) is
+// written and read with agent-scope relaxed atomics: global_store/load with
+// sc1, which write through to, and read from, the device-coherent level, so a
+// block needs no cache-wide release / acquire fence (a release fence at agent
+// scope is an L2 writeback on this chip).  Ordering, DESIGN.md §3:
+//  * writer: block stores, then drain_stores() -- s_waitcnt vmcnt(0), which
+//    returns only once every earlier store is acknowledged, written as an asm
+//    statement with a "memory" clobber so the compiler cannot move a memory
+//    access across it -- then the ring entry store (and, unpaired, the avail
+//    increment), so an entry becomes visible only after its block;
+//  * reader: the entry is loaded and its tag checked before the block's
+//    address (path id) is known, and its loads are issued after that wait.
 __device__ __forceinline__ void st_u64_h(unsigned long long *p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -163,18 +193,18 @@ __device__ __forceinline__ cf ld_cf_rlx(const cf *p) {
 __device__ __forceinline__ int ld_i_rlx(const int *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void drain_stores() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0)
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // (pointers and sizes by value: a KArgs reference would put the kernel
 // arguments in scratch memory)
-__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, int b, bool unpaired,
-                                          Workspace *ws) {
+__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch, int b,
+                                          bool unpaired, Workspace *ws) {
     const unsigned t = atomicAdd(&rq[RQ_TAIL], 1u);
     if (t >= cap) {   // cannot happen within the bound of ring_entries (the path would be lost: reported)
         atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
         return;
     }
-    st_u64_h(&ring[t], ((unsigned long long)(t + 1u) << 32) | (unsigned)b);
+    st_u64_h(&ring[t], ((unsigned long long)ring_tag(epoch, t) << 32) | (unsigned)b);
     if (unpaired) {
         drain_stores();
         atomicAdd(&rq[RQ_AVAIL], 1u);
@@ -183,19 +213,20 @@ __device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring
 // the entry of claimed ticket h: its pusher took ticket h before (head never
 // passes tail), so it is written or about to be; a pusher paused mid-push is
 // waited for (bounded: HC_ERROR_DEVICE in the status if it never comes)
-__device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigned cap, Workspace *ws, unsigned h,
-                                         const unsigned *rq) {
+__device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigned cap, unsigned epoch, Workspace *ws,
+                                         unsigned h, const unsigned *rq) {
     if (h >= cap) {
         atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
         return -1;
     }
+    const unsigned tag = ring_tag(epoch, h);
     unsigned long long e = ld_u64_h(&ring[h]);
-    if ((unsigned)(e >> 32) == h + 1u) return (int)(unsigned)e;
+    if ((unsigned)(e >> 32) == tag) return (int)(unsigned)e;
     const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
         __builtin_amdgcn_s_sleep(8);
         e = ld_u64_h(&ring[h]);
-        if ((unsigned)(e >> 32) == h + 1u) return (int)(unsigned)e;
+        if ((unsigned)(e >> 32) == tag) return (int)(unsigned)e;
         if (__builtin_amdgcn_s_memrealtime() - w0 > RING_WAIT_TICKS) break;
     }
     if (atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE) == 0u) {
@@ -208,15 +239,16 @@ __device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigne
     return -1;
 }
 __device__ __forceinline__ int ring_pop_paired(unsigned *rq, const unsigned long long *ring, unsigned cap,
-                                               Workspace *ws) {
-    return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
+                                               unsigned epoch, Workspace *ws) {
+    return ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
 }
 // oldest suspended path id, or -1 if there is none
-__device__ __forceinline__ int ring_pop(unsigned *rq, const unsigned long long *ring, unsigned cap, Workspace *ws) {
+__device__ __forceinline__ int ring_pop(unsigned *rq, const unsigned long long *ring, unsigned cap, unsigned epoch,
+                                        Workspace *ws) {
     int *avail = reinterpret_cast<int *>(&rq[RQ_AVAIL]);
     if (ld_i_rlx(avail) <= 0) return -1;
     for (;;) {
-        if (atomicSub(avail, 1) > 0) return ring_take(ring, cap, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
+        if (atomicSub(avail, 1) > 0) return ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
         if (atomicAdd(avail, 1) + 1 <= 0) return -1;
     }
 }
@@ -224,21 +256,84 @@ __device__ __forceinline__ int ring_pop(unsigned *rq, const unsigned long long *
 // ---------------------------------------------------------------- table prep
 // Compacts the reference's padded unified index (38880 ints: dH/dx at
 // ((c*8+j)*5+part)*30 + r, dH/dt at 36000 + (j*6+part)*30 + r; Data_Reader.cpp
-// :167-189, ..._LimUnroll_L2Cache.cuh:57-148) into EvalTables.  One wave,
-// lane r < 30 = equation row r.  Every index and coefficient is validated; a
-// table that does not fit sets HC_ERROR_TABLE and the tracker leaves its
-// outputs untouched.
-__global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ U, Workspace *ws,
-                                                    const uint8_t *found_in) {
+// :167-189, ..._LimUnroll_L2Cache.cuh:57-148) into EvalTables.  Lane r < 30
+// of the first wave = equation row r.  Every index and coefficient is
+// validated; a table that does not fit sets HC_ERROR_TABLE and the tracker
+// leaves its outputs untouched.  The tables persist in the workspace: a launch
+// whose index table hashes to the one they were built from (all 256 threads
+// hash it, ~10 KB each) skips the compaction.
+//
+// Also the per-launch reset of the time-slicing counters (rq != nullptr): head,
+// tail and avail zeroed, the ring epoch bumped; ring entries not cleared yet
+// (a workspace's first sliced launch, or a larger ring than before) are zeroed
+// once (hash tags never match a zero entry).
+constexpr unsigned TAB_MAGIC = 0x48435442u;   // "HCTB"
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {   // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+struct PrepArgs {
+    const int32_t *U;
+    Workspace *ws;
+    const uint8_t *found_in;     // abort mode: the (cross-rank reduced) found flag, else null
+    const unsigned *peer_found;  // abort mode: the cross-process flag, or null
+    unsigned *rq;                // time slicing, else null
+    unsigned long long *ring;
+    unsigned ring_cap;
+};
+constexpr int PREP_THREADS = 256;
+__global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
+    const int32_t *__restrict__ U = pa.U;
+    Workspace *ws = pa.ws;
     EvalTables *T = &ws->tab;
     __shared__ int s_len[32];
     __shared__ int s_bad;
-    const int r = threadIdx.x;
-    if (r == 0) {
+    __shared__ unsigned long long s_h[PREP_THREADS];
+    __shared__ unsigned s_cleared;
+    __shared__ int s_valid;
+    const int tid = threadIdx.x;
+    {
+        unsigned long long h = 0;
+#pragma unroll 8
+        for (int i = tid; i < HX_SIZE + HT_SIZE; i += PREP_THREADS)
+            h += mix64(((unsigned long long)i << 32) | (unsigned)U[i]);
+        s_h[tid] = h;
+    }
+    if (tid == 0) {
+        // the launch's control block (queue, status, flag, timestamps, diagnostics)
+        unsigned *cb = reinterpret_cast<unsigned *>(ws);
+        for (int q = 0; q < 16; q++) cb[q] = 0u;
         s_bad = 0;
-        if (found_in) ws->found = found_in[0] ? 1u : 0u;
+        if (pa.found_in) {
+            const bool peer = pa.peer_found &&
+                              __hip_atomic_load(pa.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
+            ws->found = (pa.found_in[0] || peer) ? 1u : 0u;
+        }
+        s_cleared = (pa.rq && pa.rq[RQ_MAGIC] == RQ_MAGIC_VALUE) ? pa.rq[RQ_CLEARED] : 0u;
     }
     __syncthreads();
+    for (int w = PREP_THREADS / 2; w > 0; w >>= 1) {
+        if (tid < w) s_h[tid] += s_h[tid + w];
+        __syncthreads();
+    }
+    const unsigned long long src_hash = s_h[0];
+    if (pa.rq)
+        for (unsigned e = s_cleared + tid; e < pa.ring_cap; e += PREP_THREADS) pa.ring[e] = 0ull;
+    if (tid == 0) s_valid = (T->magic == TAB_MAGIC && T->src_hash == src_hash && T->status == 0) ? 1 : 0;
+    __syncthreads();
+    if (pa.rq && tid == 0) {
+        unsigned *rq = pa.rq;
+        rq[RQ_HEAD] = 0u;
+        rq[RQ_TAIL] = 0u;
+        rq[RQ_AVAIL] = 0u;
+        const unsigned e = (rq[RQ_MAGIC] == RQ_MAGIC_VALUE) ? rq[RQ_EPOCH] + 1u : 1u;
+        rq[RQ_EPOCH] = e ? e : 1u;
+        rq[RQ_CLEARED] = s_cleared > pa.ring_cap ? s_cleared : pa.ring_cap;
+        rq[RQ_MAGIC] = RQ_MAGIC_VALUE;
+    }
+    if (s_valid) return;   // tables built from this index table already
+    const int r = tid;
     const uint2 pad_hx = make_uint2((uint32_t)(SLOT_OFF_P + 8 * 33) | ((uint32_t)(SLOT_OFF_P + 8 * 33) << 16),
                                     (uint32_t)(SLOT_OFF_X + 8 * 30) | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 8));
     if (r < 32) {
@@ -324,6 +419,8 @@ __global__ void __launch_bounds__(64) k_prep_tables(const int32_t *__restrict__ 
         for (int q = 0; q < 32; q++) mx = max(mx, s_len[q]);
         T->hx_len = mx;
         T->status = s_bad ? HC_ERROR_TABLE : 0;
+        T->src_hash = src_hash;
+        T->magic = TAB_MAGIC;
         if (s_bad) ws->status = HC_ERROR_TABLE;
     }
 }
@@ -411,6 +508,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     Workspace *ws = a.ws;
     const EvalTables *T = &ws->tab;
     if (ws->status != 0u) return;
+    // time slicing: this launch's ring epoch (bumped by k_prep_tables)
+    const unsigned epoch = (!ABORT && a.slice_q > 0) ? ld_rlx(&a.rq[RQ_EPOCH]) : 0u;
     const uint2 *s_hx = GTAB ? T->hx : reinterpret_cast<const uint2 *>(s_tab);
     const uint2 *s_ht = GTAB ? T->ht : reinterpret_cast<const uint2 *>(s_tab) + HX_SLOT_CAP * 32;
     if constexpr (!GTAB) {
@@ -491,6 +590,10 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         if ((double)r21 >= 0.90 && (double)r31 >= 0.90 && r == 0) {   // eval.cuh:241-246
                             __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             a.found_flag[0] = 1;
+                            // the other GPUs' launches poll this (system scope: written
+                            // through to the owner's memory over xGMI)
+                            if (a.peer_found)
+                                __hip_atomic_store(a.peer_found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                             a.batch_index[b] = b;
                             atomicCAS(&ws->t_found, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
                         }
@@ -515,19 +618,19 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         nb = deq_hint;                       // claimed by the suspension
                     } else if (!ABORT && deq_hint == -2) {
                         nb = a.num_paths;                    // swap: the oldest suspended path
-                        rb = ring_pop_paired(a.rq, a.ring, a.ring_cap, ws);
+                        rb = ring_pop_paired(a.rq, a.ring, a.ring_cap, epoch, ws);
                     } else {
                         nb = (ABORT || a.slice_q == 0 || ld_rlx(&ws->queue) < (unsigned)a.num_paths)
                                  ? (int)atomicAdd(&ws->queue, 1u) : a.num_paths;
-                        if (!ABORT && nb >= a.num_paths && a.slice_q > 0) rb = ring_pop(a.rq, a.ring, a.ring_cap, ws);
+                        if (!ABORT && nb >= a.num_paths && a.slice_q > 0) rb = ring_pop(a.rq, a.ring, a.ring_cap, epoch, ws);
                     }
                 }
                 deq_hint = -1;
                 nb = bperm_i(nb, hb);
                 if (!ABORT) rb = bperm_i(rb, hb);
                 if (!ABORT && rb >= 0) {
-                    // resume a suspended path at its step boundary (the state the
-                    // suspending slot stored: x in the path's own track entry)
+                    // resume a suspended path at its step boundary from its
+                    // suspend block (x in words 0..29, the scalars in 30, 31)
                     b = rb;
                     qpos = 0;
                     const int smp = b / NTRK;
@@ -540,21 +643,19 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         S.dif[r + 32] = a.diff_params[(size_t)smp * NPP + r + 32];
                     }
                     smp_loaded = smp;
-                    const cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
-                    x = rl ? ld_cf_rlx(dtrack + r) : cmk(0.0f, 0.0f);
+                    const unsigned long long *blk = a.susp + (size_t)b * SUSP_WORDS;
+                    x = rl ? ld_cf_rlx(reinterpret_cast<const cf *>(blk + r)) : cmk(0.0f, 0.0f);
                     xl = x;
                     sols = x;
-                    const unsigned long long *q = reinterpret_cast<const unsigned long long *>(a.pst + b);
-                    const unsigned long long q0 = ld_u64_h(q + 0), q1 = ld_u64_h(q + 1), q2 = ld_u64_h(q + 2),
-                                             q3 = ld_u64_h(q + 3);
+                    const unsigned long long q0 = ld_u64_h(blk + 30), q1 = ld_u64_h(blk + 31);
                     t0 = __uint_as_float((unsigned)q0);
                     dt = __uint_as_float((unsigned)(q0 >> 32));
-                    stepidx = (int)(unsigned)q1;
-                    nsteps = (int)(unsigned)(q1 >> 32);
-                    ncorr = (int)(unsigned)q2;
-                    succ = (int)(unsigned)(q2 >> 32);
-                    const int fl = (int)(unsigned)q3;
-                    end_zone = (fl & 1) != 0; check = (fl & 2) != 0; isSucc = false; isInf = false;
+                    stepidx = (int)((unsigned)q1 & 0xFFFFu);
+                    nsteps = (int)((unsigned)q1 >> 16);
+                    const unsigned w3 = (unsigned)(q1 >> 32);
+                    ncorr = (int)(w3 & 0xFFFFu);
+                    succ = (int)((w3 >> 16) & 0x3FFFu);
+                    end_zone = (w3 >> 30) & 1u; check = (w3 >> 31) & 1u; isSucc = false; isInf = false;
                     t_step = 0.0f;
                     piece = 0;
                     ph = PH_BEGIN;
@@ -567,6 +668,13 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     bool skip = false;
                     if (ABORT) {                                              // TrunRANSAC.cu:152
                         skip = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+                        if (!skip && a.peer_found &&
+                            __hip_atomic_load(a.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
+                            // another GPU found a pose: stop here too, and let the rest of
+                            // this launch see it without crossing xGMI
+                            skip = true;
+                            __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        }
                         skip = bperm_i((int)skip, hb) != 0;
                         if (skip && r == 0) {
                             a.conv[b] = 0;
@@ -640,17 +748,17 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     }
                     hint = bperm_i(hint, hb);
                     if (hint != -1) {
-                        cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
-                        if (rl) st_cf_rlx(dtrack + r, x);
-                        if (r == 0) {
-                            unsigned long long *q = reinterpret_cast<unsigned long long *>(a.pst + b);
-                            st_u64_h(q + 0, pack2(__float_as_uint(t0), __float_as_uint(dt)));
-                            st_u64_h(q + 1, pack2((unsigned)stepidx, (unsigned)nsteps));
-                            st_u64_h(q + 2, pack2((unsigned)ncorr, (unsigned)succ));
-                            st_u64_h(q + 3, pack2((unsigned)((end_zone ? 1 : 0) | (check ? 2 : 0)), 0u));
-                        }
+                        // the whole state in one 256-B block, one store per half:
+                        // lanes 0..29 x, lane 30 (t0, dt), lane 31 the counters
+                        const unsigned w2 = (unsigned)stepidx | ((unsigned)nsteps << 16);
+                        const unsigned w3 = (unsigned)ncorr | ((unsigned)succ << 16) | (end_zone ? 1u << 30 : 0u) |
+                                            (check ? 1u << 31 : 0u);
+                        const unsigned long long word =
+                            rl ? pack2(__float_as_uint(x.x), __float_as_uint(x.y))
+                               : (r == 30 ? pack2(__float_as_uint(t0), __float_as_uint(dt)) : pack2(w2, w3));
+                        st_u64_h(a.susp + (size_t)b * SUSP_WORDS + r, word);
                         drain_stores();
-                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, b, hint >= 0, ws);
+                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, epoch, b, hint >= 0, ws);
                         deq_hint = hint;
                         suspend = true;
                     } else {
@@ -734,7 +842,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         }
         HC_DIAG_MARK(0);
         // the found flag for the next step boundary: read now, used after the stage
-        if (ABORT && a.inflight_stop) found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ABORT && a.inflight_stop) {
+            found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // (the peer flag's xGMI round trip is hidden by the stage that follows)
+            if (a.peer_found) found_seen |= __hip_atomic_load(a.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
 
         // ---------------- one stage for both slots
         // park the slot state in LDS so it does not occupy VGPRs across eval + LU
@@ -772,27 +884,42 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         const bool act = ph_in == PH_STAGE;
         const bool pred = act && s_in < 4;
         HC_DIAG_MARK(1);
-        // right-hand side first: dH/dt | H need no Jacobian registers, so their
-        // LDS gathers can run many terms ahead
-        cf rB = cmk(0.0f, 0.0f);
-        if (__ballot(pred) != 0ull) {                                        // :185
-            const cf t = eval_ht(s_ht, S, r_v);
-            if (pred) rB = t;
-        }
-        if (__ballot(act && !pred) != 0ull) {                                // :221
-            const cf t = eval_h(s_ht, S, r_v);
-            if (!pred) rB = t;
-        }
-        HC_DIAG_MARK(3);
+        // the stage's linear system: right-hand side first (dH/dt | H need no
+        // Jacobian registers, so their LDS gathers can run many terms ahead),
+        // then dH/dx into rA
         cf rA[NV];
-        eval_hx(rA, s_hx, map, S, r_v);                                      // :184 / :220
-        wave_lds_sync();
+        auto build_system = [&]() -> cf {
+            cf rb = cmk(0.0f, 0.0f);
+            if (__ballot(pred) != 0ull) {                                    // :185
+                const cf t = eval_ht(s_ht, S, r_v);
+                if (pred) rb = t;
+            }
+            if (__ballot(act && !pred) != 0ull) {                            // :221
+                const cf t = eval_h(s_ht, S, r_v);
+                if (!pred) rb = t;
+            }
+            HC_DIAG_MARK(3);
+            eval_hx(rA, s_hx, map, S, r_v);                                  // :184 / :220
+            wave_lds_sync();
+            return rb;
+        };
+        const cf rB = build_system();
         HC_DIAG_MARK(2);
+        bool redo;
+        LUBuf &LB = *reinterpret_cast<LUBuf *>(S.ent);
 #ifdef HC_DIAG_LUWORK
-        const cf k = lu_solve(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent), __ballot(act));
+        cf k = lu_solve<false>(rA, rB, lane_v, row_pat, LB, redo, __ballot(act));   // :188 / :224
 #else
-        const cf k = lu_solve(rA, rB, lane_v, row_pat, *reinterpret_cast<LUBuf *>(S.ent));   // :188 / :224
+        cf k = lu_solve<false>(rA, rB, lane_v, row_pat, LB, redo);                  // :188 / :224
 #endif
+        if (__builtin_expect(redo, 0)) {
+            // a system the sparse solve cannot take exactly (an entry not provably
+            // finite, a pivot outside the fast reciprocal range): rebuilt (the
+            // evaluation is deterministic) and solved densely
+            wave_lds_sync();
+            const cf rB2 = build_system();
+            k = lu_solve<true>(rA, rB2, lane_v, row_pat, LB, redo);
+        }
         wave_lds_sync();
         HC_DIAG_MARK(5);
         {
@@ -905,7 +1032,14 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restric
         if (rA[c].x != 0.0f || rA[c].y != 0.0f) pat |= 1u << c;   // NaN counts as non-zero
     }
     const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
-    const cf x = lu_solve(rA, rB, lane, pat, s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)], __ballot(sys < n));
+    LUBuf &LB = s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)];
+    bool redo;
+    cf x = lu_solve<false>(rA, rB, lane, pat, LB, redo, __ballot(sys < n));
+    if (__builtin_expect(redo, 0)) {   // solved again densely from the original system
+#pragma unroll
+        for (int c = 0; c < NV; c++) rA[c] = ok ? A[((size_t)sys * NV + r) * NV + c] : cmk(0.0f, 0.0f);
+        x = lu_solve<true>(rA, rB, lane, pat, LB, redo);
+    }
     if (ok) X[(size_t)sys * NV + r] = x;
 }
 
@@ -953,11 +1087,12 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
 
 // ---------------------------------------------------------------- host side
 static size_t ws_bytes_needed() { return (sizeof(Workspace) + 255) & ~(size_t)255; }
-// + the time-slicing area of a launch of `paths` paths: PathState per path, then the ring
+// + the time-slicing area of a launch of `paths` paths: the ring counters, a
+// suspend block per path, then the ring
 static size_t ws_bytes_for(long long paths, int max_steps) {
     if (paths < 0) paths = 0;
     if (max_steps < 0) max_steps = 0;
-    return ws_bytes_needed() + ((RQ_WORDS * sizeof(unsigned) + (size_t)paths * sizeof(PathState) +
+    return ws_bytes_needed() + ((RQ_WORDS * sizeof(unsigned) + (size_t)paths * SUSP_WORDS * sizeof(unsigned long long) +
                                  (size_t)ring_entries(paths, max_steps) * sizeof(unsigned long long) + 255) &
                                 ~(size_t)255);
 }
@@ -1005,10 +1140,6 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     hipStream_t s = (hipStream_t)stream;
     Workspace *ws = (Workspace *)workspace;
     (void)hipGetLastError();  // errors of earlier, unrelated calls are not ours
-    if ((g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
-    hipLaunchKernelGGL(k_prep_tables, dim3(1), dim3(64), 0, s, t->unified_index, ws,
-                       abort_mode ? ab->found_trifocal_sols : nullptr);
-    if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     KArgs k{};
     k.num_paths = (int)paths;
     // abort mode dequeues sample-major, so whole hypotheses finish as early as possible
@@ -1029,20 +1160,24 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.inf = t->infinity;
     k.stats = t->stats;
     k.ws = ws;
-    // time slicing when the workspace has room for it (hc_trifocal_workspace_size_for)
+    // time slicing when the workspace has room for it (hc_trifocal_workspace_size_for) and
+    // the step counters fit the suspend block
     if (!abort_mode && SLICE_Q > 0 && wsb >= ws_bytes_for(paths, t->settings.max_steps) &&
-        ring_entries(paths, t->settings.max_steps) < 0xFFFFFF00ull) {
+        ring_entries(paths, t->settings.max_steps) < 0xFFFFFF00ull &&
+        slice_fits(t->settings.max_steps, t->settings.max_corrections, t->settings.delta_t_inc_steps)) {
         char *base = (char *)workspace + ws_bytes_needed();
         k.rq = (unsigned *)base;
-        k.pst = (PathState *)(base + RQ_WORDS * sizeof(unsigned));
-        k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) + (size_t)paths * sizeof(PathState));
+        k.susp = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned));
+        k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) +
+                                        (size_t)paths * SUSP_WORDS * sizeof(unsigned long long));
         k.ring_cap = (unsigned)ring_entries(paths, t->settings.max_steps);
         k.slice_q = SLICE_Q;
-        // counters + ring zeroed (sequence tags of an earlier launch never match)
-        if ((g_last_hip_error = hipMemsetAsync(k.rq, 0, RQ_WORDS * sizeof(unsigned), s)) != hipSuccess ||
-            (g_last_hip_error = hipMemsetAsync(k.ring, 0, sizeof(unsigned long long) * k.ring_cap, s)) != hipSuccess)
-            return HC_ERROR_LAUNCH;
     }
+    // control block reset, compacted tables (skipped when cached), ring reset
+    PrepArgs pa{t->unified_index, ws, abort_mode ? ab->found_trifocal_sols : nullptr,
+                abort_mode ? ab->peer_found : nullptr, k.rq, k.ring, k.ring_cap};
+    hipLaunchKernelGGL(k_prep_tables, dim3(1), dim3(PREP_THREADS), 0, s, pa);
+    if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     // tracking: term tables read from the workspace (L1/L2), 96 VGPRs, 27.6 KB LDS
     // per workgroup -> 5 waves/SIMD.  Abort mode keeps the tables in LDS at 4
     // waves/SIMD (the scoring path needs the registers).
@@ -1050,12 +1185,13 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     if (abort_mode && archived) return HC_ERROR_INVALID_VALUE;
     const void *kern = abort_mode ? (const void *)k_track<true, 4, false>
                        : archived ? (const void *)k_track<false, 5, true, true>
-                                  : (const void *)k_track<false, 5, true>;
+                                  : (const void *)k_track<false, HC_X_MINW, true>;
     const int grid = grid_for((int)((paths + 1) / 2), kern);
     if (grid <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
         k.num_edgels = ab->num_triplet_edgels;
         k.inflight_stop = ab->inflight_stop ? 1 : 0;
+        k.peer_found = ab->peer_found;
         k.edgels = ab->triplet_edge_locations;
         k.K = ab->intrinsic_matrix;
         k.found_flag = ab->found_trifocal_sols;
@@ -1185,8 +1321,8 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
     hipStream_t s = (hipStream_t)stream;
     hc::Workspace *ws = (hc::Workspace *)workspace;
     (void)hipGetLastError();
-    if ((hc::g_last_hip_error = hipMemsetAsync(ws, 0, 64, s)) != hipSuccess) return HC_ERROR_LAUNCH;
-    hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(64), 0, s, unified_index, ws, nullptr);
+    hc::PrepArgs pa{unified_index, ws, nullptr, nullptr, nullptr, nullptr, 0u};
+    hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(hc::PREP_THREADS), 0, s, pa);
     if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     const int per = 2 * hc::WAVES_PER_WG;
     hipLaunchKernelGGL(hc::k_eval, dim3((n + per - 1) / per), dim3(hc::WG_THREADS), 0, s, n, ws,
@@ -1196,6 +1332,47 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
 }
 
 const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip_error); }
+
+static_assert(sizeof(hcIpcHandle) == sizeof(hipIpcMemHandle_t), "hcIpcHandle mirrors hipIpcMemHandle_t");
+
+hcStatus hc_shared_flag_create(uint32_t **flag, hcIpcHandle *handle) {
+    if (!flag || !handle) return HC_ERROR_INVALID_VALUE;
+    void *p = nullptr;
+    if ((hc::g_last_hip_error = hipMalloc(&p, 256)) != hipSuccess) return HC_ERROR_DEVICE;
+    hipIpcMemHandle_t h;
+    if ((hc::g_last_hip_error = hipMemset(p, 0, 256)) != hipSuccess ||
+        (hc::g_last_hip_error = hipIpcGetMemHandle(&h, p)) != hipSuccess) {
+        (void)hipFree(p);
+        return HC_ERROR_DEVICE;
+    }
+    memcpy(handle, &h, sizeof(h));
+    *flag = (uint32_t *)p;
+    return HC_SUCCESS;
+}
+
+hcStatus hc_shared_flag_open(const hcIpcHandle *handle, uint32_t **flag) {
+    if (!flag || !handle) return HC_ERROR_INVALID_VALUE;
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    void *p = nullptr;
+    if ((hc::g_last_hip_error = hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess)) != hipSuccess)
+        return HC_ERROR_DEVICE;
+    *flag = (uint32_t *)p;
+    return HC_SUCCESS;
+}
+
+hcStatus hc_shared_flag_reset(uint32_t *flag, hcStream stream) {
+    if (!flag) return HC_ERROR_INVALID_VALUE;
+    if ((hc::g_last_hip_error = hipMemsetAsync(flag, 0, sizeof(uint32_t), (hipStream_t)stream)) != hipSuccess)
+        return HC_ERROR_LAUNCH;
+    return HC_SUCCESS;
+}
+
+hcStatus hc_shared_flag_close(uint32_t *flag, int opened) {
+    if (!flag) return HC_ERROR_INVALID_VALUE;
+    hc::g_last_hip_error = opened ? hipIpcCloseMemHandle(flag) : hipFree(flag);
+    return hc::g_last_hip_error == hipSuccess ? HC_SUCCESS : HC_ERROR_DEVICE;
+}
 
 #ifdef HC_DIAG_TIMES
 int hc_diag_span(unsigned long long *out, int reset) {

@@ -36,13 +36,15 @@
 // Exactness: a structurally zero entry holds an exact zero while no product
 // is infinite or NaN, and a - l*0 == a up to the sign of a zero.  Guarantees:
 //  * the solve runs sparse only if every entry is finite with |re|, |im| <
-//    2^64 (wave-uniform check on sums of squares; else every step is dense;
-//    the argument below needs 2^88).  Pivoting on
-//    |re|+|im| bounds every multiplier by sqrt(2) and the element growth by
-//    (1+sqrt(2))^29 < 2^37, so no intermediate can overflow;
-//  * a step whose 1/pivot leaves the fast range (|pivot| < 2^-90: 1/pivot may
-//    overflow; zero or NaN pivot) is executed densely and makes the pattern
-//    of every row below it dense.
+//    2^64 (wave-uniform check on sums of squares; the argument below needs
+//    2^88).  Pivoting on |re|+|im| bounds every multiplier by sqrt(2) and the
+//    element growth by (1+sqrt(2))^29 < 2^37, so no intermediate can overflow;
+//  * and only while every 1/pivot stays in the fast range (|pivot| < 2^-90:
+//    1/pivot may overflow; zero or NaN pivot).
+// Otherwise the sparse solve reports `redo` and the caller solves the rebuilt
+// system with the dense instantiation (every column, the IEEE reciprocal):
+// the reference algorithm step for step.  So the sparse steps carry no dense
+// tests at all (a per-step `dense` flag cost ~12 SALU and 3 branches a step).
 //
 // The buffer aliases the per-path dH/dx entry block (SlotLDS::ent), which is
 // dead between the gather of the Jacobian into registers and the next eval.
@@ -202,6 +204,35 @@ struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work cou
 #define HC_LU_WORK_PASS
 #endif
 
+#ifndef HC_X_GASM
+#define HC_X_GASM 0
+#endif
+// a_j -= l * u_j (pcmsub) for a group of 4 / 2 elements in ONE asm statement:
+// each element's second fma reads its first 4 / 2 instructions later, past the
+// packed-FP32 forwarding hazard (one wait state at distance 1), so no s_nop is
+// needed inside -- as separate statements hipcc pads the boundaries
+// conservatively
+__device__ __forceinline__ void pcmsub4(pf2 &a0, pf2 &a1, pf2 &a2, pf2 &a3, pf2 l, pf2 u0, pf2 u1, pf2 u2, pf2 u3) {
+    asm("v_pk_fma_f32 %0, %4, %5, %0 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %4, %6, %1 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %2, %4, %7, %2 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %3, %4, %8, %3 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %0, %4, %5, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %4, %6, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %2, %4, %7, %2 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %3, %4, %8, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]"
+        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
+        : "v"(l), "v"(u0), "v"(u1), "v"(u2), "v"(u3));
+}
+__device__ __forceinline__ void pcmsub2(pf2 &a0, pf2 &a1, pf2 l, pf2 u0, pf2 u1) {
+    asm("v_pk_fma_f32 %0, %2, %3, %0 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %2, %4, %1 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %0, %2, %3, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
+        "v_pk_fma_f32 %1, %2, %4, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]"
+        : "+v"(a0), "+v"(a1)
+        : "v"(l), "v"(u0), "v"(u1));
+}
+
 // a_j -= l * u_j for the groups K.. of step I (the caller is inside the
 // below-the-pivot exec region)
 template <int I, int K>
@@ -219,6 +250,20 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
 #pragma unroll
                 for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
             }
+#if HC_X_GASM
+            if constexpr (N == 4) {
+                pf2 a0 = {rA[J].x, rA[J].y}, a1 = {rA[J + 1].x, rA[J + 1].y}, a2 = {rA[J + 2].x, rA[J + 2].y},
+                    a3 = {rA[J + 3].x, rA[J + 3].y};
+                pcmsub4(a0, a1, a2, a3, pf2{l.x, l.y}, pf2{u[0].x, u[0].y}, pf2{u[1].x, u[1].y},
+                        pf2{u[2].x, u[2].y}, pf2{u[3].x, u[3].y});
+                rA[J] = cmk(a0.x, a0.y); rA[J + 1] = cmk(a1.x, a1.y);
+                rA[J + 2] = cmk(a2.x, a2.y); rA[J + 3] = cmk(a3.x, a3.y);
+            } else if constexpr (N == 2) {
+                pf2 a0 = {rA[J].x, rA[J].y}, a1 = {rA[J + 1].x, rA[J + 1].y};
+                pcmsub2(a0, a1, pf2{l.x, l.y}, pf2{u[0].x, u[0].y}, pf2{u[1].x, u[1].y});
+                rA[J] = cmk(a0.x, a0.y); rA[J + 1] = cmk(a1.x, a1.y);
+            } else
+#endif
 #pragma unroll
             for (int q = 0; q < N; q++) {
                 const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
@@ -231,17 +276,21 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
 }
 
 // The rest of pivot step I once the pivots are chosen: broadcast, relabel,
-// 1/pivot, update.  dense (a pivot outside the fast reciprocal range, or a
-// matrix not provably finite): every column group and the IEEE reciprocal.
-template <int I>
-__device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool dense, PivF &my,
-                                             LUBuf &L, bool is_piv, float piv_abs, int pl0, int pl1
-                                             HC_LU_WORK_ARG) {
-    // structural patterns of the two pivot rows (wave-uniform)
-    const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl0);
-    const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
+// 1/pivot, update.  DENSE (the whole solve of a matrix that is not provably
+// finite or that met a pivot outside the fast reciprocal range): every column
+// group and the IEEE reciprocal.  The sparse solve carries no dense tests: it
+// reports such a solve, and the caller solves the system again densely.
+template <int I, bool DENSE>
+__device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
+                                             bool is_piv, float piv_abs, int pl0, int pl1 HC_LU_WORK_ARG) {
     constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
-    const uint32_t pmw = dense ? FULL : ((pp0 | pp1) & FULL);
+    uint32_t pmw = FULL;
+    if constexpr (!DENSE) {
+        // structural patterns of the two pivot rows (wave-uniform)
+        const uint32_t pp0 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl0);
+        const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
+        pmw = (pp0 | pp1) & FULL;
+    }
     const uint32_t gb = group_bits(pmw);
     if (is_piv) {                                          // pivot row -> buffer
         L.row[I] = rA[I];
@@ -259,7 +308,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
     cf reg;
     divf f;
-    if (__builtin_expect(!dense, 1)) {
+    if constexpr (!DENSE) {
         pf2 oo;
         const pf2 rg = recip_fast(pf2{sxi.x, sxi.y}, piv_abs, oo);
         reg = cmk(rg.x, rg.y);
@@ -277,33 +326,29 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // one exec-masked region per step: multiplier, right-hand side,
     // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
     // below whose column I may be non-zero takes the pivot patterns (both
-    // halves': a superset of its own pivot row's); after a dense step
-    // nothing is known zero.
-    // dense step: every row below becomes dense (a uniform branch, taken
-    // rarely; asm keeps it from being if-converted into a per-step select)
-    if (__builtin_expect(dense, 0)) {
-        if (below) asm volatile("v_mov_b32 %0, -1" : "=v"(pat));
-    }
+    // halves': a superset of its own pivot row's).
     if (below) {
         const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
         const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
         rB = cmk(bp.x, bp.y);
-        // v_bfe_i32 + v_and_or_b32 (after a dense step pat is all ones already)
-        pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
+        // v_bfe_i32 + v_and_or_b32
+        if constexpr (!DENSE) pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
         lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
     }
 }
 
-template <int I>
-__device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, bool all_dense, int lane,
-                                           int r, int hb, bool row_lane, PivF &my, LUBuf &L HC_LU_WORK_ARG) {
+// One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
+// outside the fast reciprocal range sets `redo` (the solve goes on with
+// garbage, the caller discards it and solves densely).
+template <int I, bool DENSE>
+__device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
+                                           bool row_lane, PivF &my, LUBuf &L, bool &redo HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
         const bool elig = rowid >= I && row_lane;
         bool is_piv;
         float piv_abs;
         int pl0, pl1;   // pivot lanes of the two halves
-        bool dense;
         const int key = elig ? __float_as_int(v) : -1;
         const int mx = half_max_int_p16(key);
         const unsigned long long m = __builtin_amdgcn_ballot_w64(key == mx);
@@ -311,7 +356,7 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
         // common: one maximum per half (two in the wave; s_bcnt1, where the
         // per-half m & (m - 1) tests took six SALU), both in the fast range
-        const bool rare = (__builtin_popcountll(m) != 2) | (bad != 0ull) | all_dense;
+        const bool rare = DENSE || (__builtin_popcountll(m) != 2) | (bad != 0ull);
         if (__builtin_expect(rare, 0)) {
             // rare: NaN at position I wins (:57-64); exact ties: first position wins
             const bool isn = v != v;
@@ -331,16 +376,16 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             const unsigned long long pm = __builtin_amdgcn_ballot_w64(is_piv);
             pl0 = __builtin_ctz((unsigned)pm | 0x80000000u);
             pl1 = 32 + __builtin_ctz((unsigned)(pm >> 32) | 0x80000000u);
-            dense = all_dense || __builtin_amdgcn_ballot_w64(!rcp_fast_bits(__float_as_int(piv_abs))) != 0ull;
+            if constexpr (!DENSE)
+                redo = redo || __builtin_amdgcn_ballot_w64(!rcp_fast_bits(__float_as_int(piv_abs))) != 0ull;
         } else {
             is_piv = key == mx;
             piv_abs = __int_as_float(mx);
             pl0 = __builtin_ctz(mlo);        // exactly one bit per half here
             pl1 = 32 + __builtin_ctz(mhi);
-            dense = false;
         }
-        lu_step_body<I>(rA, rB, rowid, pat, dense, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
-        lu_forward<I + 1>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L HC_LU_WORK_PASS);
+        lu_step_body<I, DENSE>(rA, rB, rowid, pat, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
+        lu_forward<I + 1, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo HC_LU_WORK_PASS);
     }
 }
 
@@ -380,38 +425,49 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 
 // Solves the system of each half: lane r holds row r of A in rA and b_r in
 // rB; pattern = the structural pattern of row r.  Returns x_r in lane r.  L is
-// this half's buffer (16-B aligned).
-__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L,
+// this half's buffer (16-B aligned).  DENSE = false: the structurally sparse
+// solve, which sets `redo` (wave-uniform) instead of handling a matrix that is
+// not provably finite or a pivot outside the fast reciprocal range: the
+// caller then rebuilds the system and calls the DENSE solve, the reference
+// algorithm step for step (both exact).
+template <bool DENSE>
+__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, bool &redo,
                                       unsigned long long count_mask = ~0ull) {
     (void)count_mask;   // diagnostic builds (HC_DIAG_LUWORK): lanes whose executed work is counted
-    // every entry finite and below 2^64 in magnitude (inside the 2^88 the
-    // sparse path needs): the per-component sums of squares (v_pk_fma_f32, 30
-    // VALU) stay finite only then -- NaN propagates, an inf or |entry| >= 2^64
-    // makes a square overflow.  A sum that overflows from many entries below
-    // 2^64 only sends the solve to the dense path, which is exact as well.
-    pf2 sq = {0.0f, 0.0f};
-#pragma unroll
-    for (int c = 0; c < NV; c++) {
-        const pf2 e = {rA[c].x, rA[c].y};
-        asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(sq) : "v"(e));
-    }
-    const bool ok = sq.x + sq.y < __builtin_inff();
-    const bool all_dense = __builtin_amdgcn_ballot_w64(!ok) != 0ull;   // then every step is dense
     const int r = lane & 31, hb = lane & 32;
     const bool row_lane = r < NV;
+    redo = false;
+    if constexpr (!DENSE) {
+        // every entry finite and below 2^64 in magnitude (inside the 2^88 the
+        // sparse path needs): the per-component sums of squares (v_pk_fma_f32, 30
+        // VALU) stay finite only then -- NaN propagates, an inf or |entry| >= 2^64
+        // makes a square overflow.  A sum that overflows from many entries below
+        // 2^64 only sends the solve to the dense path, which is exact as well.
+        pf2 sq = {0.0f, 0.0f};
+#pragma unroll
+        for (int c = 0; c < NV; c++) {
+            const pf2 e = {rA[c].x, rA[c].y};
+            asm("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(sq) : "v"(e));
+        }
+        const bool ok = sq.x + sq.y < __builtin_inff();
+        if (__builtin_expect(__builtin_amdgcn_ballot_w64(!ok) != 0ull, 0)) {
+            redo = true;
+            return cmk(0.0f, 0.0f);
+        }
+    }
     int rowid = row_lane ? r : 99;   // padding lanes never pivot
     uint32_t pat = row_lane ? pattern : 0u;
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
     LuWork lu_work_acc{0ull, count_mask};
-    lu_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L, lu_work_acc);
+    lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
-    if (lane == 0) {
+    if (lane == 0 && !redo) {
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
         atomicAdd(&g_diag_luwork[1], solves);
     }
 #else
-    lu_forward<0>(rA, rB, rowid, pat, all_dense, lane, r, hb, row_lane, my, L);
+    lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
 #endif
     lu_backward<NV - 1>(rA, rB, rowid, my);
     // lane r returns x_r: the owner of position r holds it in rB

@@ -30,6 +30,8 @@ static void usage() {
            "      --share-devices  allow more GPUs (-g) than devices: logical GPU g runs on device g %% count\n"
            "      --inflight-stop  abort mode: paths in flight also stop once a pose is found\n"
            "                    (Abort_Inflight_Stop; default: they run to completion as in the reference)\n"
+           "      --abort-across-gpus  abort mode: one found flag shared by all GPUs (Abort_Across_GPUs;\n"
+           "                    default: one flag per GPU as in the reference)\n"
            "      --write-sols  write Output_Write_Files/GPU_Converged_HC_tracks.txt\n"
            "      --quirks      reference-literal pose selection (Pose_Selection_Reference_Quirks)\n"
            "  -s, --dataset     RANSAC dataset directory name (default Synthetic)\n");
@@ -38,7 +40,8 @@ static void usage() {
 int main(int argc, char **argv) {
     std::string problem, root = "../../";
     int samples = -1, gpus = -1, times = 1;
-    bool abort_flag = false, write_sols = false, quirks = false, inflight_stop = false, share = false;
+    bool abort_flag = false, write_sols = false, quirks = false, inflight_stop = false, share = false,
+         across = false;
     std::string dataset;
     if (argc <= 1) { usage(); return 0; }
     for (int i = 1; i < argc; i++) {
@@ -55,6 +58,7 @@ int main(int argc, char **argv) {
         else if (a == "-t" || a == "--times") times = std::stoi(next("-t"));
         else if (a == "--abort") abort_flag = true;
         else if (a == "--inflight-stop") inflight_stop = true;
+        else if (a == "--abort-across-gpus") across = true;
         else if (a == "--share-devices") share = true;
         else if (a == "--write-sols") write_sols = true;
         else if (a == "--quirks") quirks = true;
@@ -73,6 +77,7 @@ int main(int argc, char **argv) {
         if (gpus > 0) s.set("Num_Of_GPUs", std::to_string(gpus));
         if (abort_flag) s.set("Abort_RANSAC_by_Good_Sol", "true");
         if (inflight_stop) s.set("Abort_Inflight_Stop", "true");
+        if (across) s.set("Abort_Across_GPUs", "true");
         if (share) s.set("Share_Devices", "true");
         if (write_sols) s.set("Write_Converged_Sols", "true");
         if (quirks) s.set("Pose_Selection_Reference_Quirks", "true");

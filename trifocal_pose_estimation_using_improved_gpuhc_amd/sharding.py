@@ -17,6 +17,13 @@ data path needs no collective.  RCCL carries only:
     covered every rank's paths (gather_pose_selection);
   * timing (barrier, max / min over ranks) in bench.py.
 
+With a SharedFlag (hcAbortArgs::peer_found) the stop no longer waits for a
+chunk boundary: the flag lives in one rank's device memory, every other rank
+maps it (hipIpcOpenMemHandle over xGMI), a launch sets it with a system-scope
+store when it finds a pose and polls it before every path it starts (with
+inflight_stop also at every step boundary).  The chunk-boundary reduction
+stays as the fallback and for the found bytes the host reads.
+
 The reference has no cross-GPU early stop: each GPU keeps its own flag
 (GPU_HC_Solver.cpp:308-333).  With one rank the protocol reduces to the
 reference behaviour.
@@ -123,3 +130,89 @@ def gather_pose_selection(selection, path_offset: int, group=None, quirks: bool 
     offs = [torch.empty_like(off) for _ in range(world)]
     dist.all_gather(offs, off, group=group)
     return pose.merge([p.cpu().numpy() for p in parts], [int(o.item()) for o in offs], quirks)
+
+
+class SharedFlag:
+    """The cross-process early-stop flag of a multi-GPU abort run
+    (hcAbortArgs::peer_found; include/hc_trifocal.h hc_shared_flag_*).
+
+    Rank `owner` of `group` allocates it in its device memory; the 64-byte IPC
+    handle is broadcast over torch.distributed (a CPU tensor for gloo, a device
+    tensor for RCCL) and every other rank maps it with hipIpcOpenMemHandle.
+    Construction is collective.  If any rank cannot create or map it, every
+    rank gets .ptr = None (the chunk-boundary reduction alone then stops the
+    run) and .error says why."""
+
+    def __init__(self, group=None, owner: int = 0, device=None):
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+
+        from . import _abi
+        self._L = _abi.lib()
+        self.ptr = None
+        self.opened = False
+        self.error = None
+        rank = dist.get_rank(group)
+        src = dist.get_global_rank(group, owner) if group is not None else owner
+        on_gpu = dist.get_backend(group) == "nccl"
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        handle = _abi.hcIpcHandle()
+        p = C.c_void_p()
+        ok = 1
+        if rank == owner:
+            st = self._L.hc_shared_flag_create(C.byref(p), C.byref(handle))
+            if st != 0:
+                ok, self.error = 0, f"hc_shared_flag_create: {_abi.HC_STATUS.get(st, st)}"
+        buf = torch.tensor(list(bytes(handle.reserved)), dtype=torch.uint8, device=dev if on_gpu else "cpu")
+        dist.broadcast(buf, src=src, group=group)
+        if rank != owner:
+            C.memmove(handle.reserved, bytes(buf.cpu().tolist()), 64)
+            st = self._L.hc_shared_flag_open(C.byref(handle), C.byref(p))
+            if st != 0:
+                ok, self.error = 0, f"hc_shared_flag_open: {_abi.HC_STATUS.get(st, st)} " \
+                                    f"({self._L.hc_last_error_string().decode(errors='replace')})"
+            else:
+                self.opened = True
+        agree = torch.tensor([ok], dtype=torch.int32, device=dev if on_gpu else "cpu")
+        dist.all_reduce(agree, op=dist.ReduceOp.MIN, group=group)
+        if int(agree.item()) == 1:
+            self.ptr = p.value
+        elif p.value:
+            self._L.hc_shared_flag_close(C.c_void_p(p.value), 1 if self.opened else 0)
+            self.error = self.error or "another rank could not map the flag"
+        self._group = group
+        self._owner = owner
+        self._rank = rank
+
+    def arm(self, stream=None) -> None:
+        """Zeroes the flag before a run: the owner resets and synchronises, then
+        all ranks pass a barrier, so no launch starts before the reset."""
+        import ctypes as C
+
+        import torch
+        import torch.distributed as dist
+        if self.ptr is None:
+            return
+        if self._rank == self._owner:
+            s = stream if stream is not None else torch.cuda.current_stream()
+            st = self._L.hc_shared_flag_reset(C.c_void_p(self.ptr), C.c_void_p(s.cuda_stream))
+            if st != 0:
+                raise RuntimeError(f"hc_shared_flag_reset failed: {st}")
+            s.synchronize()
+        dist.barrier(group=self._group)
+
+    def close(self) -> None:
+        """Collective: the mapping ranks unmap before the owner frees."""
+        import ctypes as C
+
+        import torch.distributed as dist
+        if self.ptr is None:
+            return
+        if self.opened:
+            self._L.hc_shared_flag_close(C.c_void_p(self.ptr), 1)
+        dist.barrier(group=self._group)
+        if not self.opened:
+            self._L.hc_shared_flag_close(C.c_void_p(self.ptr), 0)
+        self.ptr = None

@@ -102,7 +102,8 @@ class DeviceTracker:
     def launch(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, abort: bool = False,
                stream: torch.cuda.Stream | None = None, workspace: torch.Tensor | None = None,
                sample_offset: int = 0, num_samples: int | None = None, inflight_stop: bool = False,
-               truncate: bool = True, explicit_rk: bool = False, time_slicing: bool = True) -> None:
+               truncate: bool = True, explicit_rk: bool = False, time_slicing: bool = True,
+               peer_found=None) -> None:
         """Enqueue one tracking run on `stream` (no synchronisation).
 
         Samples [sample_offset, sample_offset + num_samples) of `target`/`diff`
@@ -113,6 +114,8 @@ class DeviceTracker:
         they run to completion).  truncate=False: no depth-sign path
         truncation (the archived ..._PH_CodeOpt kernel, hc_trifocal_2op1p_30x30_track_ph_codeopt);
         with explicit_rk=True as well, the archived ..._PH kernel (hc_trifocal_2op1p_30x30_track_ph).
+        peer_found (abort mode): a sharding.SharedFlag of a multi-GPU run
+        (hcAbortArgs::peer_found): set here on a find, polled before each path.
         time_slicing (tracking launches): suspend and resume paths at step
         boundaries so every path starts early (hc_trifocal_workspace_size_for;
         bit-identical results).  The default workspace grows to the size that
@@ -168,6 +171,7 @@ class DeviceTracker:
             ab.found_trifocal_sols = r.found.data_ptr()
             ab.trifocal_sols_batch_index = r.batch_index[p0:p1].data_ptr()
             ab.inflight_stop = 1 if inflight_stop else 0
+            ab.peer_found = None if peer_found is None else peer_found.ptr
             _abi.check(self.L.hc_trifocal_2op1p_30x30_track_abort(C.byref(a), C.byref(ab), ws, wsb, hs),
                        "hc_trifocal_2op1p_30x30_track_abort")
         elif explicit_rk:
@@ -189,11 +193,13 @@ class DeviceTracker:
 
     def launch_abort_chunked(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, chunk_samples: int,
                              workspaces: list, group=None, stream: torch.cuda.Stream | None = None,
-                             inflight_stop: bool = False) -> list:
+                             inflight_stop: bool = False, peer_found=None) -> list:
         """Abort-mode run of all of target's samples in chunks, with the
         cross-rank early-stop flag (sharding.run_abort_chunks): the launches
         and the flag reductions share one stream.  workspaces: one per chunk
-        (grown as needed).  Returns the (offset, count) chunks."""
+        (grown as needed).  peer_found: a sharding.SharedFlag, so the launches
+        also stop on another rank's find within a path (not only at the next
+        chunk boundary).  Returns the (offset, count) chunks."""
         from . import sharding
         parts = sharding.chunks(target.shape[0], chunk_samples)
         while len(workspaces) < len(parts):
@@ -202,7 +208,7 @@ class DeviceTracker:
 
         def one(k, off, n):
             self.launch(target, diff, r, abort=True, stream=s, workspace=workspaces[k], sample_offset=off,
-                        num_samples=n, inflight_stop=inflight_stop)
+                        num_samples=n, inflight_stop=inflight_stop, peer_found=peer_found)
         sharding.run_abort_chunks(one, r.found, target.shape[0], chunk_samples, group=group, stream=s)
         return parts
 
