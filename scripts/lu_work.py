@@ -8,6 +8,7 @@ path slots below the pivot).  The dense algorithm (the reference's) updates
 sum_{I} (29 - I)^2 = 8555 elements per solve; the structurally sparse LU skips
 column groups that are zero in both pivot rows of a wave.  Prints the executed
 fraction for one config-2 launch; bench.py prices the LU's update FLOPs with it.
+Also counts the solves the sparse LU handed to the dense re-solve (round 3).
 """
 import ctypes as C
 import json
@@ -29,7 +30,7 @@ def main():
     L = _abi.lib()
     fn = L.hc_diag_luwork
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    out = (C.c_ulonglong * 2)()
+    out = (C.c_ulonglong * 3)()
     dev = torch.device("cuda:0")
     problem = load_problem()
     tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, 100)
@@ -43,9 +44,10 @@ def main():
     fn(out, 1)
     st = r.stats.cpu().numpy()
     stages = 4 * int(st[:, 0].sum()) + int(st[:, 1].sum())
-    elems, solves = int(out[0]), int(out[1])
+    elems, solves, dense = int(out[0]), int(out[1]), int(out[2])
     res = {"config": "config 2 (100 samples, abort off), one launch",
            "solves_counted": solves, "path_stages": stages,
+           "solves_rerun_densely": dense,
            "executed_update_elements": elems,
            "executed_update_elements_per_solve": elems / max(1, solves),
            "dense_update_elements_per_solve": DENSE_UPDATE_ELEMENTS,

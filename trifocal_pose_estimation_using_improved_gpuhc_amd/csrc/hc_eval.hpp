@@ -105,9 +105,6 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
 // ahead of the previous terms' entry stores (which the compiler may not move
 // loads across), so a lane has several terms' LDS reads in flight instead of
 // one round trip per term, with few registers held.
-#ifndef HC_X_EPAIR
-#define HC_X_EPAIR 0
-#endif
 constexpr int EV_AHEAD = 2;
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
@@ -140,7 +137,7 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
             if (r < NV) *reinterpret_cast<pf2 *>(eb + 8 * hx_gslot(k)) = acc;   // (padding lanes alias row 0)
             acc = pf2{0.0f, 0.0f};
         }
-        if (!HC_X_EPAIR || (k & 1)) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -149,14 +146,9 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
 // so several terms' LDS reads stay in flight; each entry slot is stored once,
 // where its group of terms ends, slot 6 (structural zero) is zeroed, and 30
 // gathers through the column -> slot map rebuild the register row.
-__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t (&map)[3], SlotLDS &S,
-                                        int r) {
-    cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
-    eval_hx_terms(s_hx, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
-    float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    if (r < NV) ent_row[6] = cmk(z, z);   // structural zero (the LU reuses this block)
-    wave_lds_sync();
+// the register row r of dH/dx from the lane's entry block (S.ent row r)
+__device__ __forceinline__ void gather_hx(cf (&rA)[NV], const uint32_t (&map)[3], const SlotLDS &S, int r) {
+    const cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
     // opaque copy: keeps LICM from hoisting the 30 decoded gather addresses out
     // of the path loop (30 VGPRs held across the LU, then spilled)
     uint32_t m[3] = {map[0], map[1], map[2]};
@@ -169,6 +161,17 @@ __device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const u
         asm("v_bfe_u32 %0, %1, %2, 3" : "=v"(code) : "v"(m[c / 10]), "i"(3 * (c % 10)));
         rA[c] = *reinterpret_cast<const cf *>(eb + (code << 3));
     }
+}
+
+__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t (&map)[3], SlotLDS &S,
+                                        int r) {
+    cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
+    eval_hx_terms(s_hx, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
+    float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    if (r < NV) ent_row[6] = cmk(z, z);   // structural zero
+    wave_lds_sync();
+    gather_hx(rA, map, S, r);
 }
 
 struct HtOps { pf2 pa, pb, da, db, xu, xv, xw; };
@@ -198,7 +201,7 @@ __device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r
         s = s * pf2{co, co};
         const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
         acc = pcmsub(acc, P, q.xw);
-        if (!HC_X_EPAIR || (j & 1)) __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
+        __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
     }
     return cmk(acc.x, acc.y);
 }
@@ -228,7 +231,7 @@ __device__ __forceinline__ cf eval_h(const uint2 *s_ht, const SlotLDS &S, int r)
         pf2 P = q.pa * pf2{co, co};
         P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
         acc = pcmadd(acc, P, q.xw);
-        if (!HC_X_EPAIR || (j & 1)) __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_sched_barrier(0);
     }
     return cmk(acc.x, acc.y);
 }

@@ -90,13 +90,7 @@ static_assert(offsetof(Workspace, tab) == 64, "control block is 64 bytes");
 // word 31 = (stepidx | nsteps << 16, ncorr | succ << 16 | flags << 30); the
 // launcher enables slicing only where these fields fit (slice_fits).
 constexpr int SUSP_WORDS = 32;
-#ifndef HC_X_MINW
-#define HC_X_MINW 5
-#endif
-#ifndef HC_X_SLICE_Q
-#define HC_X_SLICE_Q 3
-#endif
-constexpr int SLICE_Q = HC_X_SLICE_Q;          // steps per time slice (profiles/r2n_ab_slice*.jsonl)
+constexpr int SLICE_Q = 3;          // steps per time slice (profiles/r2n_ab_slice*.jsonl, r3d_ab.jsonl)
 __host__ __device__ constexpr bool slice_fits(int max_steps, int max_corr, int inc_steps) {
     return max_steps >= 0 && max_steps < 16000 && inc_steps >= 0 && inc_steps < 16384 && max_corr >= 0 &&
            (long long)max_corr * (max_steps + 2) < 65536;
@@ -887,26 +881,22 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         // the stage's linear system: right-hand side first (dH/dt | H need no
         // Jacobian registers, so their LDS gathers can run many terms ahead),
         // then dH/dx into rA
+        cf rB = cmk(0.0f, 0.0f);
+        if (__ballot(pred) != 0ull) {                                        // :185
+            const cf t = eval_ht(s_ht, S, r_v);
+            if (pred) rB = t;
+        }
+        if (__ballot(act && !pred) != 0ull) {                                // :221
+            const cf t = eval_h(s_ht, S, r_v);
+            if (!pred) rB = t;
+        }
+        HC_DIAG_MARK(3);
         cf rA[NV];
-        auto build_system = [&]() -> cf {
-            cf rb = cmk(0.0f, 0.0f);
-            if (__ballot(pred) != 0ull) {                                    // :185
-                const cf t = eval_ht(s_ht, S, r_v);
-                if (pred) rb = t;
-            }
-            if (__ballot(act && !pred) != 0ull) {                            // :221
-                const cf t = eval_h(s_ht, S, r_v);
-                if (!pred) rb = t;
-            }
-            HC_DIAG_MARK(3);
-            eval_hx(rA, s_hx, map, S, r_v);                                  // :184 / :220
-            wave_lds_sync();
-            return rb;
-        };
-        const cf rB = build_system();
+        eval_hx(rA, s_hx, map, S, r_v);                                      // :184 / :220
+        wave_lds_sync();
         HC_DIAG_MARK(2);
         bool redo;
-        LUBuf &LB = *reinterpret_cast<LUBuf *>(S.ent);
+        LUBuf &LB = *reinterpret_cast<LUBuf *>(S.lu);
 #ifdef HC_DIAG_LUWORK
         cf k = lu_solve<false>(rA, rB, lane_v, row_pat, LB, redo, __ballot(act));   // :188 / :224
 #else
@@ -914,11 +904,20 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 #endif
         if (__builtin_expect(redo, 0)) {
             // a system the sparse solve cannot take exactly (an entry not provably
-            // finite, a pivot outside the fast reciprocal range): rebuilt (the
-            // evaluation is deterministic) and solved densely
-            wave_lds_sync();
-            const cf rB2 = build_system();
-            k = lu_solve<true>(rA, rB2, lane_v, row_pat, LB, redo);
+            // finite, a pivot outside the fast reciprocal range): the Jacobian is
+            // re-gathered from the entry block (which the solve leaves intact),
+            // the right-hand side re-evaluated, and the system solved densely
+            cf rb = cmk(0.0f, 0.0f);
+            if (__ballot(pred) != 0ull) {
+                const cf t = eval_ht(s_ht, S, r_v);
+                if (pred) rb = t;
+            }
+            if (__ballot(act && !pred) != 0ull) {
+                const cf t = eval_h(s_ht, S, r_v);
+                if (!pred) rb = t;
+            }
+            gather_hx(rA, map, S, r_v);
+            k = lu_solve<true>(rA, rb, lane_v, row_pat, LB, redo);
         }
         wave_lds_sync();
         HC_DIAG_MARK(5);
@@ -1185,7 +1184,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     if (abort_mode && archived) return HC_ERROR_INVALID_VALUE;
     const void *kern = abort_mode ? (const void *)k_track<true, 4, false>
                        : archived ? (const void *)k_track<false, 5, true, true>
-                                  : (const void *)k_track<false, HC_X_MINW, true>;
+                                  : (const void *)k_track<false, 5, true>;
     const int grid = grid_for((int)((paths + 1) / 2), kern);
     if (grid <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
@@ -1233,9 +1232,9 @@ int hc_diag_phases(unsigned long long *out, int reset) {
 
 #ifdef HC_DIAG_LUWORK
 int hc_diag_luwork(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_luwork), sizeof(unsigned long long) * 2) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_luwork), sizeof(unsigned long long) * 3) != hipSuccess) return -1;
     if (reset) {
-        static const unsigned long long z[2] = {0, 0};
+        static const unsigned long long z[3] = {0, 0, 0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_luwork), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -46,8 +46,8 @@
 // the reference algorithm step for step.  So the sparse steps carry no dense
 // tests at all (a per-step `dense` flag cost ~12 SALU and 3 branches a step).
 //
-// The buffer aliases the per-path dH/dx entry block (SlotLDS::ent), which is
-// dead between the gather of the Jacobian into registers and the next eval.
+// The buffer is the path slot's SlotLDS::lu; the dH/dx entry block (SlotLDS::ent)
+// survives the solve, so a dense re-solve re-gathers the Jacobian from it.
 #pragma once
 
 #include "hc_eval.hpp"
@@ -59,8 +59,8 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 struct alignas(16) LUBuf {
     cf row[32];    // current pivot row: [0..29] A, [30] rhs, [31].x = rowid (int bits); x in the back sub
 };
-static_assert(sizeof(LUBuf) <= sizeof(cf) * NV * 7, "LUBuf must fit in SlotLDS::ent");
-static_assert(offsetof(SlotLDS, ent) % 16 == 0, "SlotLDS::ent must be 16-B aligned");
+static_assert(sizeof(LUBuf) == sizeof(SlotLDS::lu), "LUBuf is SlotLDS::lu");
+static_assert(offsetof(SlotLDS, lu) % 16 == 0, "SlotLDS::lu must be 16-B aligned");
 
 constexpr int LU_CHUNK = 4;   // columns per skippable group (even)
 
@@ -192,7 +192,7 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uin
 #ifdef HC_DIAG_LUWORK
 // diagnostic build: rank-1 update elements the solves execute (sum over the
 // executed column groups of columns x active lanes), and the solves
-__device__ unsigned long long g_diag_luwork[2];
+__device__ unsigned long long g_diag_luwork[3];   // executed elements, sparse solves, solves re-run densely
 struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work counts (active path slots)
 #define HC_LU_WORK(ncols) (lu_work_acc.acc += (unsigned long long)(ncols) * \
     (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask))
@@ -203,35 +203,6 @@ struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work cou
 #define HC_LU_WORK_ARG
 #define HC_LU_WORK_PASS
 #endif
-
-#ifndef HC_X_GASM
-#define HC_X_GASM 0
-#endif
-// a_j -= l * u_j (pcmsub) for a group of 4 / 2 elements in ONE asm statement:
-// each element's second fma reads its first 4 / 2 instructions later, past the
-// packed-FP32 forwarding hazard (one wait state at distance 1), so no s_nop is
-// needed inside -- as separate statements hipcc pads the boundaries
-// conservatively
-__device__ __forceinline__ void pcmsub4(pf2 &a0, pf2 &a1, pf2 &a2, pf2 &a3, pf2 l, pf2 u0, pf2 u1, pf2 u2, pf2 u3) {
-    asm("v_pk_fma_f32 %0, %4, %5, %0 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %1, %4, %6, %1 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %2, %4, %7, %2 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %3, %4, %8, %3 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %0, %4, %5, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %1, %4, %6, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %2, %4, %7, %2 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %3, %4, %8, %3 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]"
-        : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3)
-        : "v"(l), "v"(u0), "v"(u1), "v"(u2), "v"(u3));
-}
-__device__ __forceinline__ void pcmsub2(pf2 &a0, pf2 &a1, pf2 l, pf2 u0, pf2 u1) {
-    asm("v_pk_fma_f32 %0, %2, %3, %0 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %1, %2, %4, %1 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %0, %2, %3, %0 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
-        "v_pk_fma_f32 %1, %2, %4, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]"
-        : "+v"(a0), "+v"(a1)
-        : "v"(l), "v"(u0), "v"(u1));
-}
 
 // a_j -= l * u_j for the groups K.. of step I (the caller is inside the
 // below-the-pivot exec region)
@@ -250,20 +221,6 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
 #pragma unroll
                 for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
             }
-#if HC_X_GASM
-            if constexpr (N == 4) {
-                pf2 a0 = {rA[J].x, rA[J].y}, a1 = {rA[J + 1].x, rA[J + 1].y}, a2 = {rA[J + 2].x, rA[J + 2].y},
-                    a3 = {rA[J + 3].x, rA[J + 3].y};
-                pcmsub4(a0, a1, a2, a3, pf2{l.x, l.y}, pf2{u[0].x, u[0].y}, pf2{u[1].x, u[1].y},
-                        pf2{u[2].x, u[2].y}, pf2{u[3].x, u[3].y});
-                rA[J] = cmk(a0.x, a0.y); rA[J + 1] = cmk(a1.x, a1.y);
-                rA[J + 2] = cmk(a2.x, a2.y); rA[J + 3] = cmk(a3.x, a3.y);
-            } else if constexpr (N == 2) {
-                pf2 a0 = {rA[J].x, rA[J].y}, a1 = {rA[J + 1].x, rA[J + 1].y};
-                pcmsub2(a0, a1, pf2{l.x, l.y}, pf2{u[0].x, u[0].y}, pf2{u[1].x, u[1].y});
-                rA[J] = cmk(a0.x, a0.y); rA[J + 1] = cmk(a1.x, a1.y);
-            } else
-#endif
 #pragma unroll
             for (int q = 0; q < N; q++) {
                 const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
@@ -466,6 +423,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
         atomicAdd(&g_diag_luwork[1], solves);
     }
+    if (lane == 0 && !DENSE && redo) atomicAdd(&g_diag_luwork[2], solves);   // solves re-run densely
 #else
     lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
 #endif

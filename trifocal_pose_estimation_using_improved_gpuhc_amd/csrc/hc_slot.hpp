@@ -28,7 +28,8 @@ struct alignas(16) SlotLDS {
     cf p[NPP];       // p(t)
     cf tgt[NPP];     // target params
     cf dif[NPP];     // diff params
-    cf ent[NV * 7];  // dH/dx entries of row r at [r*7 + slot], slot 6 = 0; the LU's pivot-row buffer
+    cf ent[NV * 7];  // dH/dx entries of row r at [r*7 + slot], slot 6 = 0 (kept through the LU)
+    cf lu[32];       // the LU's pivot-row buffer (hc_lu.hpp LUBuf)
     SlotState st;
     char bank_pad[16];   // slot stride = 16 mod 256 B: the slots of one wave (same offsets,
                          // different bases) land on different LDS banks
