@@ -267,7 +267,8 @@ def main():
                     dist.barrier()
                 w0 = time.perf_counter()
                 tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream, inflight_stop=inflight,
-                                        peer_found=peer if peer is not None and peer.ptr is not None else None)
+                                        peer_found=peer if peer is not None and peer.ptr is not None else None,
+                                        max_count=sharding.max_shard(Sa * world, world))
                 torch.cuda.synchronize(dev)
                 w = time.perf_counter() - w0
                 hz = tr.read_timestamps(wss[0])[2]

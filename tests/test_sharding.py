@@ -53,7 +53,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, total, chunk, passing, out_dir):
+def _worker(rank, world, port, total, chunk, passing, out_dir, use_max=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -67,15 +67,16 @@ def _worker(rank, world, port, total, chunk, passing, out_dir):
                 if any(off + o <= s < off + o + n for s in passing):
                     flag.fill_(1)
 
-        nchunks = sharding.run_abort_chunks(launch_chunk, flag, cnt, chunk)
+        nchunks = sharding.run_abort_chunks(launch_chunk, flag, cnt, chunk,
+                                            max_count=sharding.max_shard(total, world) if use_max else None)
         np.save(os.path.join(out_dir, f"r{rank}.npy"), np.array([nchunks, int(flag.item())] + worked, np.int64))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, total, chunk, passing, tmp_path):
-    mp.start_processes(_worker, args=(world, _free_port(), total, chunk, passing, str(tmp_path)), nprocs=world,
-                       join=True, start_method="fork")
+def _run(world, total, chunk, passing, tmp_path, use_max=False):
+    mp.start_processes(_worker, args=(world, _free_port(), total, chunk, passing, str(tmp_path), use_max),
+                       nprocs=world, join=True, start_method="fork")
     return [np.load(os.path.join(tmp_path, f"r{r}.npy")).tolist() for r in range(world)]
 
 
@@ -113,6 +114,19 @@ def test_uneven_chunk_counts_do_not_hang(tmp_path):
     res = _run(2, 17, 8, [8], tmp_path)              # global sample 8 = rank 0's second chunk
     assert [r[1] for r in res] == [1, 1]
     assert [r[2:] for r in res] == [[0, 1], [0]]
+
+
+@pytest.mark.timeout(120)
+def test_max_count_agrees_without_a_host_read(tmp_path):
+    """With max_count (every rank knows the largest shard, sharding.max_shard)
+    the ranks agree on the number of flag reductions without the extra
+    all_reduce + host read: same chunks, same stop, no hang on uneven shards."""
+    assert sharding.max_shard(17, 2) == 9 and sharding.max_shard(16, 2) == 8 and sharding.max_shard(5, 8) == 1
+    res = _run(2, 17, 8, [8], tmp_path, use_max=True)
+    assert [r[0] for r in res] == [2, 1] and [r[1] for r in res] == [1, 1]
+    assert [r[2:] for r in res] == [[0, 1], [0]]
+    res = _run(3, 80, 10, [55], tmp_path, use_max=True)   # shards 27 / 27 / 26, the pass in rank 2's chunk 0
+    assert all(r[1] == 1 for r in res)
 
 
 def _pose_worker(rank, world, port, cuts, out_dir):

@@ -53,16 +53,19 @@ def chunks(count: int, chunk_samples: int) -> List[Tuple[int, int]]:
 
 
 def run_abort_chunks(launch_chunk: Callable[[int, int, int], None], flag, count: int, chunk_samples: int,
-                     group=None, stream=None) -> int:
+                     group=None, stream=None, max_count: int | None = None) -> int:
     """Early-stop protocol over this rank's samples.
 
     launch_chunk(k, offset, n) enqueues chunk k (samples [offset, offset+n) of
     the shard); the launch reads `flag` when it starts and sets it when a
     passing hypothesis is found.  After each launch the flag is max-reduced
     over all ranks.  Every rank makes the same number of reductions -- the
-    largest chunk count over the ranks (one extra all_reduce agrees on it), so
-    a rank whose shard is a chunk shorter (uneven sample counts) pads with
-    reductions that launch nothing instead of leaving its peers waiting.  With
+    largest chunk count over the ranks, so a rank whose shard is a chunk
+    shorter (uneven sample counts) pads with reductions that launch nothing
+    instead of leaving its peers waiting.  The caller that knows the largest
+    shard (max_count: every rank computes shard() of every rank) passes it and
+    nothing synchronises with the host; without it one extra all_reduce agrees
+    on the count (a host read).  With
     RCCL the reductions and the launches are ordered on `stream` (the launch
     stream; default: the current stream), so nothing synchronises with the
     host between chunks; with gloo they are synchronous.  Returns the number
@@ -79,7 +82,9 @@ def run_abort_chunks(launch_chunk: Callable[[int, int, int], None], flag, count:
     ctx = torch.cuda.stream(stream) if (on_gpu and stream is not None) else contextlib.nullcontext()
     with ctx:
         rounds = len(parts)
-        if multi:
+        if multi and max_count is not None:
+            rounds = max(rounds, len(chunks(max_count, chunk_samples)))
+        elif multi:
             n = torch.tensor([rounds], dtype=torch.int64, device=flag.device)
             dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
             rounds = int(n.item())
@@ -89,6 +94,12 @@ def run_abort_chunks(launch_chunk: Callable[[int, int, int], None], flag, count:
             if multi:
                 dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
     return len(parts)
+
+
+def max_shard(num_samples: int, world: int) -> int:
+    """The largest shard of num_samples over world ranks (rank 0's: the first
+    num_samples % world ranks take one extra sample)."""
+    return shard(num_samples, world, 0)[1]
 
 
 def first_found_seconds(stamps: List[Tuple[int, int]], tick_hz: float) -> float:

@@ -193,13 +193,15 @@ class DeviceTracker:
 
     def launch_abort_chunked(self, target: torch.Tensor, diff: torch.Tensor, r: TrackResult, chunk_samples: int,
                              workspaces: list, group=None, stream: torch.cuda.Stream | None = None,
-                             inflight_stop: bool = False, peer_found=None) -> list:
+                             inflight_stop: bool = False, peer_found=None, max_count: int | None = None) -> list:
         """Abort-mode run of all of target's samples in chunks, with the
         cross-rank early-stop flag (sharding.run_abort_chunks): the launches
         and the flag reductions share one stream.  workspaces: one per chunk
         (grown as needed).  peer_found: a sharding.SharedFlag, so the launches
         also stop on another rank's find within a path (not only at the next
-        chunk boundary).  Returns the (offset, count) chunks."""
+        chunk boundary).  max_count: the largest shard over the ranks
+        (sharding.max_shard), so the chunk count needs no host-side agreement.
+        Returns the (offset, count) chunks."""
         from . import sharding
         parts = sharding.chunks(target.shape[0], chunk_samples)
         while len(workspaces) < len(parts):
@@ -209,7 +211,8 @@ class DeviceTracker:
         def one(k, off, n):
             self.launch(target, diff, r, abort=True, stream=s, workspace=workspaces[k], sample_offset=off,
                         num_samples=n, inflight_stop=inflight_stop, peer_found=peer_found)
-        sharding.run_abort_chunks(one, r.found, target.shape[0], chunk_samples, group=group, stream=s)
+        sharding.run_abort_chunks(one, r.found, target.shape[0], chunk_samples, group=group, stream=s,
+                                  max_count=max_count)
         return parts
 
     def workspace_status(self, workspace: torch.Tensor | None = None) -> None:
