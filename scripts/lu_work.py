@@ -9,6 +9,9 @@ sum_{I} (29 - I)^2 = 8555 elements per solve; the structurally sparse LU skips
 column groups that are zero in both pivot rows of a wave.  Prints the executed
 fraction for one config-2 launch; bench.py prices the LU's update FLOPs with it.
 Also counts the solves the sparse LU handed to the dense re-solve (round 3).
+--scaled: the input of tests/test_gpu_parity.py::test_tracker_dense_resolve_
+matches_oracle instead (sample 0 and its target parameters x 2^40 and x 2^70),
+to show that test reaches the dense re-solve.
 """
 import ctypes as C
 import json
@@ -34,8 +37,12 @@ def main():
     dev = torch.device("cuda:0")
     problem = load_problem()
     tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, 100)
+    scaled = "--scaled" in sys.argv[1:]
+    if scaled:
+        tgt = np.stack([tgt[0]] + [(tgt[0] * np.float32(s)).astype(np.float32) for s in (2.0 ** 40, 2.0 ** 70)])
+        dif = (tgt - problem.start_params[None]).astype(np.float32)
     tr = DeviceTracker(problem, dev)
-    r = tr.allocate(100)
+    r = tr.allocate(tgt.shape[0])
     tr.reset_tracks(r)
     torch.cuda.synchronize()
     fn(out, 1)
@@ -45,7 +52,8 @@ def main():
     st = r.stats.cpu().numpy()
     stages = 4 * int(st[:, 0].sum()) + int(st[:, 1].sum())
     elems, solves, dense = int(out[0]), int(out[1]), int(out[2])
-    res = {"config": "config 2 (100 samples, abort off), one launch",
+    res = {"config": ("sample 0 of config 2 + its target params x 2^40, x 2^70 (one launch)" if scaled
+                      else "config 2 (100 samples, abort off), one launch"),
            "solves_counted": solves, "path_stages": stages,
            "solves_rerun_densely": dense,
            "executed_update_elements": elems,

@@ -141,6 +141,33 @@ def test_tracker_matches_oracle_small(problem, oracle, samples100, tracker):
     assert (r["tracks"][:, 30, 0] == 1.0).all()
 
 
+def test_tracker_dense_resolve_matches_oracle(problem, oracle, samples100, tracker):
+    """The tracker's dense re-solve (hc_lu.hpp lu_solve<true>, taken when a
+    Jacobian entry reaches 2^64 or a pivot leaves the fast-reciprocal range):
+    config 2 never takes it (profiles/r3e_lu_work.json), so this run forces it.
+    Sample 0 is config 2's, samples 1 and 2 have their target parameters scaled
+    by 2^40 and 2^70: their Jacobians pass 2^64 within the first steps (2^70:
+    at t = 0.01 already, max |entry| 7.5e36) and most paths run to infinity.
+    Because the dequeue is track-major, waves pair a normal path with a scaled
+    one, so a normal half is re-solved densely beside a scaled half (the redo is
+    wave-uniform) and must come out identical.  Bit-exact against the oracle."""
+    tgt, dif, _ = samples100
+    T = [tgt[0]]
+    for sc in (2.0 ** 40, 2.0 ** 70):
+        T.append((tgt[0] * np.float32(sc)).astype(np.float32))
+    T = np.stack(T)
+    D = (T - problem.start_params[None]).astype(np.float32)   # prepare_target_params' diff
+    assert np.array_equal(D[0], dif[0])
+    r = tracker.track(T, D).host()
+    tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, T, D, problem.unified_index)
+    assert (r["converge"] == conv).all() and (r["infinity"] == inf).all()
+    assert (r["stats"]["steps"] == st["steps"]).all()
+    assert (r["stats"]["corrections"] == st["corrections"]).all()
+    bad = ~same(r["tracks"][:, :30], tr[:, :30]).all(axis=(1, 2))
+    assert not bad.any(), f"{bad.sum()} tracks differ, first {np.nonzero(bad)[0][:5]}"
+    assert inf[312:].sum() > 600 and conv[:312].sum() > 0   # the scaled samples diverge, sample 0 converges
+
+
 def test_tracker_matches_golden_N100(problem, samples100, tracker):
     """Config 2 (100 samples, abort off): every flag / count / track hash equals the committed golden run."""
     import sys
