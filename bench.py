@@ -40,10 +40,10 @@ FLOP_CORR_STAGE = 101.3e3    # Hx 12,276 + H 10,080 + LU 78,670 + update/norms ~
 # The LU's rank-1 updates are 8555 element updates (8 FLOP each = 68,440 FLOP)
 # of the 78,670 in the dense algorithm the reference runs.  The structurally
 # sparse LU executes only the column groups that are non-zero in a pivot row
-# of the wave: 5,063.5 elements per solve on config 2 (0.592 of dense), measured
-# by the HC_DIAG_LUWORK build (scripts/lu_work.py, profiles/r3e_lu_work.json).
+# of the wave: 5,040.1 elements per solve on config 2 (0.589 of dense), measured
+# by the HC_DIAG_LUWORK build (scripts/lu_work.py, profiles/r3j_lu_work.json).
 LU_UPDATE_DENSE_FLOP = 68440.0
-LU_UPDATE_EXECUTED_FRACTION = 0.5919
+LU_UPDATE_EXECUTED_FRACTION = 0.5891
 LU_EXEC_SAVING = LU_UPDATE_DENSE_FLOP * (1.0 - LU_UPDATE_EXECUTED_FRACTION)
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak (64 FLOP/clk/SIMD) == FP32 MFMA peak
 HBM_PEAK_GBS = 8000.0
@@ -354,8 +354,8 @@ def main():
                                  "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = FLOPs of "
                                  "the executed stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 kFLOP / "
                                  "corrector stage, with the LU's rank-1 updates counted over the column groups "
-                                 "the structurally sparse LU executes: 0.592 of the dense 68.4 kFLOP, "
-                                 "profiles/r3e_lu_work.json) / median single-launch kernel time (HIP events on "
+                                 "the structurally sparse LU executes: 0.589 of the dense 68.4 kFLOP, "
+                                 "profiles/r3j_lu_work.json) / median single-launch kernel time (HIP events on "
                                  "the launch stream). achieved_dense_lu prices the LU as the reference's dense "
                                  "algorithm.",
                          "kernel_ms": round(float(np.median(launch_ms)), 4),

@@ -54,8 +54,10 @@ def main():
     elems, solves, dense = int(out[0]), int(out[1]), int(out[2])
     res = {"config": ("sample 0 of config 2 + its target params x 2^40, x 2^70 (one launch)" if scaled
                       else "config 2 (100 samples, abort off), one launch"),
-           "solves_counted": solves, "path_stages": stages,
+           "sparse_solves_completed": solves, "path_stages": stages,
            "solves_rerun_densely": dense,
+           "check": "sparse_solves_completed + solves_rerun_densely == path_stages",
+           "check_ok": solves + dense == stages,
            "executed_update_elements": elems,
            "executed_update_elements_per_solve": elems / max(1, solves),
            "dense_update_elements_per_solve": DENSE_UPDATE_ELEMENTS,

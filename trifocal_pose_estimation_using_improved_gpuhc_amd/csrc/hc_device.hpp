@@ -67,6 +67,14 @@ __device__ __forceinline__ cf cdiv_apply(cf x, const divf &f) {
 
 // ------------------------------------------------------------------ lanes
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
+// The lane id computed where it is used (v_mbcnt on an opaque all-ones mask):
+// LICM cannot hoist it out of the tracker's path loop, where the register
+// allocator would spill it and reload it from scratch every stage.
+__device__ __forceinline__ int lane_fresh() {
+    unsigned m = ~0u;
+    asm volatile("" : "+s"(m));
+    return (int)__builtin_amdgcn_mbcnt_hi(m, __builtin_amdgcn_mbcnt_lo(m, 0u));
+}
 
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
@@ -115,6 +123,8 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return __builtin_amdgcn_readfirstlane(v);
 }
 __device__ __forceinline__ int bperm_i(int v, int src_lane) { return __builtin_amdgcn_ds_bpermute(src_lane << 2, v); }
+// lane 0 of each 32-lane half to the whole half (address from lane_fresh)
+__device__ __forceinline__ int bcast_half0(int v) { return __builtin_amdgcn_ds_bpermute((lane_fresh() & 32) << 2, v); }
 // broadcast relative lane L (compile-time) of each 32-lane half to the whole half
 template <int L>
 __device__ __forceinline__ float hbcast_f(float v) {

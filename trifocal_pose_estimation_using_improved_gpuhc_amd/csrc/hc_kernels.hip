@@ -90,7 +90,14 @@ static_assert(offsetof(Workspace, tab) == 64, "control block is 64 bytes");
 // word 31 = (stepidx | nsteps << 16, ncorr | succ << 16 | flags << 30); the
 // launcher enables slicing only where these fields fit (slice_fits).
 constexpr int SUSP_WORDS = 32;
-constexpr int SLICE_Q = 3;          // steps per time slice (profiles/r2n_ab_slice*.jsonl, r3d_ab.jsonl)
+// Steps per time slice: SLICE_Q while at most one suspended path per path slot
+// waits (the launch's end, where the rotation's granularity sets the tail;
+// profiles/r2n_ab_slice*.jsonl, r3d_ab_lu_slicing.jsonl), SLICE_QBIG while
+// more wait (round 3: as fair a rotation with fewer hand-overs, 239 vs 339 MB
+// of HBM traffic per config-2 launch at the same launch time;
+// profiles/r3g_ab_quantum.jsonl, r3h_ab_quantum.jsonl).
+constexpr int SLICE_Q = 3;
+constexpr int SLICE_QBIG = 8;
 __host__ __device__ constexpr bool slice_fits(int max_steps, int max_corr, int inc_steps) {
     return max_steps >= 0 && max_steps < 16000 && inc_steps >= 0 && inc_steps < 16384 && max_corr >= 0 &&
            (long long)max_corr * (max_steps + 2) < 65536;
@@ -620,8 +627,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     }
                 }
                 deq_hint = -1;
-                nb = bperm_i(nb, hb);
-                if (!ABORT) rb = bperm_i(rb, hb);
+                nb = bcast_half0(nb);
+                if (!ABORT) rb = bcast_half0(rb);
                 if (!ABORT && rb >= 0) {
                     // resume a suspended path at its step boundary from its
                     // suspend block (x in words 0..29, the scalars in 30, 31)
@@ -669,7 +676,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                             skip = true;
                             __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         }
-                        skip = bperm_i((int)skip, hb) != 0;
+                        skip = bcast_half0((int)skip) != 0;
                         if (skip && r == 0) {
                             a.conv[b] = 0;
                             a.inf[b] = 0;
@@ -738,10 +745,16 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                             const int t = (int)atomicAdd(&ws->queue, 1u);
                             if (t < a.num_paths) hint = t;
                         }
-                        if (hint < 0 && ld_i_rlx(reinterpret_cast<const int *>(&a.rq[RQ_AVAIL])) > 0) hint = -2;
+                        if (hint < 0) {
+                            // -3: suspended paths wait, but more than one per path
+                            // slot and this slice is shorter than SLICE_QBIG: go on
+                            const int av = ld_i_rlx(reinterpret_cast<const int *>(&a.rq[RQ_AVAIL]));
+                            const int slots = (int)(gridDim.x * (WG_THREADS / WAVE) * 2u);
+                            if (av > 0) hint = (piece >= SLICE_QBIG || av <= slots) ? -2 : -3;
+                        }
                     }
-                    hint = bperm_i(hint, hb);
-                    if (hint != -1) {
+                    hint = bcast_half0(hint);
+                    if (hint >= 0 || hint == -2) {
                         // the whole state in one 256-B block, one store per half:
                         // lanes 0..29 x, lane 30 (t0, dt), lane 31 the counters
                         const unsigned w2 = (unsigned)stepidx | ((unsigned)nsteps << 16);
@@ -755,7 +768,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, epoch, b, hint >= 0, ws);
                         deq_hint = hint;
                         suspend = true;
-                    } else {
+                    } else if (hint == -1) {
                         piece = 0;
                     }
                 }
@@ -859,9 +872,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             const bool pred0 = act0 && s < 4;
             if (pred0 && r < NPP - 1) {                                      // :181 p(t), i < 33
                 const float omt = (float)(1.0 - (double)t0);
-                const cf *sp = s_sp;   // opaque base: the address is not hoisted and held across the loop
-                asm volatile("" : "+v"(sp));
-                S.p[r] = cadd(cscale(S.tgt[r], t0), cscale(sp[r], omt));
+                const int rs = lane_fresh() & 31;   // == r; the LDS address is not hoisted and held across the loop
+                S.p[r] = cadd(cscale(S.tgt[r], t0), cscale(s_sp[rs], omt));
             }
             if (pred0 && r == 0) S.p[32] = cadd(cscale(S.tgt[32], t0), cscale(s_sp[32], (float)(1.0 - (double)t0)));
         }
@@ -870,8 +882,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         asm volatile("" :: "v"(s_in), "v"(ph_in));
         // opaque lane id: keeps LICM from hoisting ~30 lane-derived per-pivot
         // constants (bpermute addresses, r == i masks) out of the path loop
-        int lane_v = lane_id();   // recomputed (2 VALU), not held across the loop
-        asm volatile("" : "+v"(lane_v));
+        const int lane_v = lane_fresh();   // recomputed (2 VALU), not held across the loop
         const int r_v = lane_v & 31;
         const uint32_t map[3] = {s_rowc[0][r_v], s_rowc[1][r_v], s_rowc[2][r_v]};
         const uint32_t row_pat = s_rowc[3][r_v];
@@ -907,17 +918,24 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             // finite, a pivot outside the fast reciprocal range): the Jacobian is
             // re-gathered from the entry block (which the solve leaves intact),
             // the right-hand side re-evaluated, and the system solved densely
+            // (the stage kind re-read from the parked slot state: held across the
+            // LU, act / pred would be spilled)
+            const bool act_r = S.st.ph == PH_STAGE, pred_r = act_r && S.st.s < 4;
             cf rb = cmk(0.0f, 0.0f);
-            if (__ballot(pred) != 0ull) {
+            if (__ballot(pred_r) != 0ull) {
                 const cf t = eval_ht(s_ht, S, r_v);
-                if (pred) rb = t;
+                if (pred_r) rb = t;
             }
-            if (__ballot(act && !pred) != 0ull) {
+            if (__ballot(act_r && !pred_r) != 0ull) {
                 const cf t = eval_h(s_ht, S, r_v);
-                if (!pred) rb = t;
+                if (!pred_r) rb = t;
             }
             gather_hx(rA, map, S, r_v);
+#ifdef HC_DIAG_LUWORK
+            k = lu_solve<true>(rA, rb, lane_v, row_pat, LB, redo, __ballot(act_r));
+#else
             k = lu_solve<true>(rA, rb, lane_v, row_pat, LB, redo);
+#endif
         }
         wave_lds_sync();
         HC_DIAG_MARK(5);
@@ -933,9 +951,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             xl = rl ? S.xl[r] : cmk(0.0f, 0.0f);
             sols = rl ? S.sols[r] : cmk(0.0f, 0.0f);
         }
-        if (act) {
+        // act / pred of this stage, from the reloaded state
+        const bool act_q = ph == PH_STAGE, pred_q = act_q && s < 4;
+        if (act_q) {
             bool step_end = false;
-            if (pred) {
+            if (pred_q) {
                 if (ARCH && s < 3 && a.explicit_rk) {
                     // archived ..._PH.cu with dev-get-new-data.cuh:37-71, gc = MAGMA_C_ONE:
                     // s += ((k*dt)*gc*1.0)/(6|3); x = (s ? x_last : x) + k*((h2|dt)*gc)

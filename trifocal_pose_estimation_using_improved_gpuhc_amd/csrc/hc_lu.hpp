@@ -192,7 +192,7 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uin
 #ifdef HC_DIAG_LUWORK
 // diagnostic build: rank-1 update elements the solves execute (sum over the
 // executed column groups of columns x active lanes), and the solves
-__device__ unsigned long long g_diag_luwork[3];   // executed elements, sparse solves, solves re-run densely
+__device__ unsigned long long g_diag_luwork[3];   // executed elements and completed sparse solves; dense solves
 struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work counts (active path slots)
 #define HC_LU_WORK(ncols) (lu_work_acc.acc += (unsigned long long)(ncols) * \
     (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask))
@@ -419,11 +419,11 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     LuWork lu_work_acc{0ull, count_mask};
     lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
-    if (lane == 0 && !redo) {
+    if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
         atomicAdd(&g_diag_luwork[1], solves);
     }
-    if (lane == 0 && !DENSE && redo) atomicAdd(&g_diag_luwork[2], solves);   // solves re-run densely
+    if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
     lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
 #endif
