@@ -128,7 +128,11 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
         if (k + EV_WAHEAD < HX_SLOT_CAP) w[k + EV_WAHEAD] = s_hx[(k + EV_WAHEAD) * 32 + r];
         if (k + EV_AHEAD < HX_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
         const HxOps &q = o[k % (EV_AHEAD + 1)];
-        const float co = (float)(int)(int8_t)(uint8_t)(w[k].y >> 16);
+        // (float)(int8_t)(w.y >> 16) in one SDWA convert (the compiler's form
+        // took a v_alignbit first)
+        float co;
+        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2"
+            : "=v"(co) : "v"(w[k].y));
         pf2 P = q.pa * pf2{co, co};
         P = pcmul(P, q.pb);
         P = pcmul(P, q.xu);

@@ -349,9 +349,12 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
 // back substitution (:97-106): the lane whose final rowid is I owns position I
 // and divides with the factors it kept from the forward step; x_I reaches the
 // lanes of its half with v_readlane (owner lane of each half found by a
-// ballot of the final row ids)
+// ballot of the final row ids), and lanes I and 32 + I -- which return x_I --
+// capture it with one exec-masked move (static lanes: no compare, no select,
+// no LDS redistribution at the end).  The owner's rB is final at its step:
+// later steps J < I update only rows at positions below J.
 template <int I>
-__device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my) {
+__device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, pf2 &res) {
     if constexpr (I >= 0) {
         const unsigned long long own = __builtin_amdgcn_ballot_w64(rowid == I);
         const int o0 = __builtin_ctz((unsigned)own);          // one owner per half
@@ -362,21 +365,20 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
         const float x1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.x), o1));
         const float y1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q.y), o1));
         // x_I of each half from its SGPR pair: one v_mov_b64 for all lanes, one
-        // more with the low half masked off (exec_lo saved and restored; the
-        // tracker's solves run with full exec) -- instead of 4 v_mov + 2 v_cndmask
+        // more with the low half masked off, one into res of lanes I, 32 + I
+        // (exec saved and restored)
         const pf2 xs0 = {x0, y0}, xs1 = {x1, y1};
         pf2 xv;
-        unsigned tmp;
-        asm volatile("s_nop 1\n\tv_mov_b64 %0, %2\n\ts_mov_b32 %1, exec_lo\n\ts_mov_b32 exec_lo, 0\n\t"
-                     "v_mov_b64 %0, %3\n\ts_mov_b32 exec_lo, %1"
-                     : "=&v"(xv), "=&s"(tmp) : "s"(xs0), "s"(xs1));
-        const cf xi = cmk(xv.x, xv.y);
+        unsigned long long tmp;
+        asm volatile("s_nop 1\n\ts_mov_b64 %2, exec\n\tv_mov_b64 %0, %3\n\ts_mov_b32 exec_lo, 0\n\t"
+                     "v_mov_b64 %0, %4\n\ts_mov_b32 exec_lo, %5\n\ts_mov_b32 exec_hi, %5\n\t"
+                     "v_mov_b64 %1, %0\n\ts_mov_b64 exec, %2"
+                     : "=&v"(xv), "+v"(res), "=&s"(tmp) : "s"(xs0), "s"(xs1), "i"(1u << I));
         if (rowid < I) {
-            const pf2 w = pcmsub(pf2{rB.x, rB.y}, pf2{xi.x, xi.y}, pf2{rA[I].x, rA[I].y});
+            const pf2 w = pcmsub(pf2{rB.x, rB.y}, xv, pf2{rA[I].x, rA[I].y});
             rB = cmk(w.x, w.y);
         }
-        if (rowid == I) rB = xi;   // the owner keeps its x_I (returned below)
-        lu_backward<I - 1>(rA, rB, rowid, my);
+        lu_backward<I - 1>(rA, rB, rowid, my, res);
     }
 }
 
@@ -427,12 +429,10 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
 #else
     lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
 #endif
-    lu_backward<NV - 1>(rA, rB, rowid, my);
-    // lane r returns x_r: the owner of position r holds it in rB
-    wave_lds_sync();
-    if (row_lane) L.row[rowid] = rB;
-    wave_lds_sync();
-    return L.row[row_lane ? r : 0];
+    // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
+    pf2 res = {0.0f, 0.0f};
+    lu_backward<NV - 1>(rA, rB, rowid, my, res);
+    return cmk(res.x, res.y);
 }
 
 }  // namespace hc
