@@ -16,7 +16,9 @@
 //    accumulator (dH/dx) or to the finished sum (dH/dt, H; the reference also
 //    evaluates its padding terms);
 //  * dH/dx terms are grouped by entry into slots of fixed capacity (below), so
-//    every entry ends at a compile-time term position on every lane.
+//    every entry ends at a compile-time term position on every lane; the
+//    entries are packed over all 32 lanes of a half (any lane may compute any
+//    row's entry), not one row per lane.
 #pragma once
 
 #include <stddef.h>
@@ -27,16 +29,23 @@ namespace hc {
 
 typedef float pf2 __attribute__((ext_vector_type(2)));
 
-// dH/dx terms grouped by entry: a row's entries sorted by their number of
-// terms (largest first) go to entry slots 0..5, slot s holding at most
-// HX_GCAP[s] terms (this problem's maxima over the rows: 8, 5, 5, 5, 1, 1).
-// Every lane's entries then end at the same static term positions, so the
-// term loop stores each entry once, at compile-time positions, instead of a
-// running sum per term (6 stores instead of 24, no per-term address or reset
-// selects).  Shorter entries are padded with coefficient-0 terms on unit
-// operands (p[33] = x[30] = 1), as the reference pads its 8-term lists.
-constexpr int HX_GCAP[6] = {8, 5, 5, 5, 1, 1};
-constexpr int HX_SLOT_CAP = 25;
+// dH/dx terms grouped by entry.  A Jacobian entry (one row, one column: the
+// sum of its 1..8 terms, in table order) is computed by one lane of the half
+// in one of its entry slots; slot s holds at most HX_GCAP[s] terms.  Since
+// every lane stores its slot s at the same compile-time term position, the
+// term loop has one store per slot (no per-term address or reset selects);
+// shorter entries are padded with coefficient-0 terms on unit operands
+// (p[33] = x[30] = 1), as the reference pads its 8-term lists.  The 170
+// entries of this problem (12 x 8, 8 x 6, 36 x 5, 4 x 4, 54 x 3, 56 x 1
+// terms) are bin-packed by k_prep_tables over all 32 lanes, so the loop is
+// 21 terms long (8 + 5 + 3 + 3 + 1 + 1) instead of the 25 that one row per
+// lane needs (rows of 11 to 23 terms in slots of 8, 5, 5, 5, 1, 1).  An entry
+// goes to its row's block in SlotLDS::ent at the byte offset the lane's
+// destination word holds for that slot (unused slots: the LU buffer's last
+// word, which the LU rewrites before it reads it).
+constexpr int HX_GCAP[6] = {8, 5, 3, 3, 1, 1};
+constexpr int HX_SLOT_CAP = 21;
+constexpr int HX_NSLOT = 6;
 __host__ __device__ constexpr int hx_gend(int s) { return s < 0 ? 0 : hx_gend(s - 1) + HX_GCAP[s]; }   // end of slot s
 __host__ __device__ constexpr bool hx_is_gend(int k) {
     return k + 1 == hx_gend(0) || k + 1 == hx_gend(1) || k + 1 == hx_gend(2) || k + 1 == hx_gend(3) ||
@@ -49,14 +58,19 @@ static_assert(hx_gend(5) == HX_SLOT_CAP, "slot capacities");
 constexpr int SLOT_OFF_X = (int)offsetof(SlotLDS, x);
 constexpr int SLOT_OFF_P = (int)offsetof(SlotLDS, p);
 constexpr int SLOT_DIF_DELTA = (int)offsetof(SlotLDS, dif) - (int)offsetof(SlotLDS, p);
+constexpr int SLOT_OFF_ENT = (int)offsetof(SlotLDS, ent);
+constexpr int SLOT_OFF_HXDUMMY = (int)offsetof(SlotLDS, lu) + 8 * 31;   // unused entry slots store here
+static_assert(SLOT_OFF_ENT + 8 * NV * 7 < 65536 && SLOT_OFF_HXDUMMY < 65536, "entry offsets must fit 16 bits");
 static_assert(SLOT_OFF_X + 8 * 31 < 256, "x offsets must fit a byte");
 static_assert(SLOT_OFF_P + 8 * NPP < 65536, "p offsets must fit 16 bits");
 
 // Compacted tables, built once per launch by k_prep_tables from the
 // reference's padded unified index (Data_Reader.cpp:167-189).
-//  map[q][r]  (row r): column c -> entry slot (3 bits x 10 columns per word, 6 = structural zero)
-//  hx[k][r] (row r's k-th dH/dx term, entry slot hx_gslot(k)): .x = off(p[a]) | off(p[b]) << 16
+//  map[q][r]  (row r): column c -> entry slot of row r's block in SlotLDS::ent
+//             (3 bits x 10 columns per word, 6 = structural zero)
+//  hx[k][l] (lane l's k-th dH/dx term, entry slot hx_gslot(k)): .x = off(p[a]) | off(p[b]) << 16
 //                                      .y = off(x[u]) | off(x[v]) << 8 | (int8)coef << 16
+//  hxd[q][l]  (lane l): SlotLDS byte offsets its slots 2q (bits 0..15) and 2q+1 (bits 16..31) store to
 //  ht[j][r] (row r's j-th dH/dt / H term): .x = off(p[a]) | off(p[b]) << 16
 //                                      .y = off(x[u]) | off(x[v]) << 8 | off(x[w]) << 16 | (int8)coef << 24
 struct EvalTables {
@@ -67,6 +81,7 @@ struct EvalTables {
     unsigned long long src_hash;      // hash of the unified index they were built from
     unsigned long long pad2;
     uint32_t map[3][32];
+    uint32_t hxd[HX_NSLOT / 2][32];
     uint2 hx[HX_SLOT_CAP * 32];
     uint2 ht[HT_TERMS * 32];
 };
@@ -114,9 +129,12 @@ __device__ __forceinline__ HxOps hx_ops(const char *sb, uint2 w) {
 }
 
 // the term loop of eval_hx: operands are read through sb (x, p of the slot),
-// running sums written through eb (the lane's entry row)
-__device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb, char *eb, int r) {
+// each finished entry is stored at sb + the lane's destination offset
+__device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const uint32_t *s_hxd, char *sb, int r) {
     uint2 w[HX_SLOT_CAP];
+    uint32_t dst[HX_NSLOT / 2];
+#pragma unroll
+    for (int q = 0; q < HX_NSLOT / 2; q++) dst[q] = s_hxd[q * 32 + r];
 #pragma unroll
     for (int k = 0; k < EV_WAHEAD; k++) w[k] = s_hx[k * 32 + r];
     HxOps o[EV_AHEAD + 1];
@@ -137,8 +155,10 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const char *sb,
         P = pcmul(P, q.pb);
         P = pcmul(P, q.xu);
         acc = pcmadd(acc, P, q.xv);
-        if (hx_is_gend(k)) {                 // static: the entry of slot hx_gslot(k) ends here on every lane
-            if (r < NV) *reinterpret_cast<pf2 *>(eb + 8 * hx_gslot(k)) = acc;   // (padding lanes alias row 0)
+        if (hx_is_gend(k)) {                 // static: the entry in slot hx_gslot(k) ends here on every lane
+            const int sl = hx_gslot(k);
+            const uint32_t off = (sl & 1) ? (dst[sl >> 1] >> 16) : (dst[sl >> 1] & 0xFFFFu);
+            *reinterpret_cast<pf2 *>(sb + off) = acc;
             acc = pf2{0.0f, 0.0f};
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -167,10 +187,10 @@ __device__ __forceinline__ void gather_hx(cf (&rA)[NV], const uint32_t (&map)[3]
     }
 }
 
-__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t (&map)[3], SlotLDS &S,
-                                        int r) {
+__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t *s_hxd,
+                                        const uint32_t (&map)[3], SlotLDS &S, int r) {
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
-    eval_hx_terms(s_hx, reinterpret_cast<const char *>(&S), reinterpret_cast<char *>(ent_row), r);
+    eval_hx_terms(s_hx, s_hxd, reinterpret_cast<char *>(&S), r);
     float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
     if (r < NV) ent_row[6] = cmk(z, z);   // structural zero
@@ -206,6 +226,41 @@ __device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r
         const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
         acc = pcmsub(acc, P, q.xw);
         __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
+    }
+    return cmk(acc.x, acc.y);
+}
+
+// dH/dt in the halves with ht_half, H in the others, in one pass: for a wave
+// whose two paths run different stage kinds (predictor | corrector: 44 % of
+// the wave-stages of config 2), instead of both full loops.  A term's x part
+// ((prefix * x[u]) * x[v], accumulated with x[w]) is the same in both; the
+// prefix is per half:
+//   dH/dt: -(c * (d[a]*p[b] + d[b]*p[a])), negated so that the accumulation
+//          is acc + P*x[w] in both (acc - P*x[w] == acc + (-P)*x[w] bit for
+//          bit, and the negation passes through the products exactly);
+//   H:     (c * p[a]) * p[b].
+__device__ __forceinline__ cf eval_hth(const uint2 *s_ht, const SlotLDS &S, int r, bool ht_half) {
+    const char *sb = reinterpret_cast<const char *>(&S);
+    uint2 w[HT_TERMS];
+#pragma unroll
+    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht[j * 32 + r];
+    HtOps o[EV_AHEAD + 1];
+#pragma unroll
+    for (int j = 0; j < EV_AHEAD; j++) o[j] = ht_ops(sb, w[j]);
+    pf2 acc = {0.0f, 0.0f};
+#pragma unroll
+    for (int j = 0; j < HT_TERMS; j++) {
+        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht[(j + EV_WAHEAD) * 32 + r];
+        if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = ht_ops(sb, w[j + EV_AHEAD]);
+        const HtOps &q = o[j % (EV_AHEAD + 1)];
+        const float co = (float)((int)w[j].y >> 24);
+        pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
+        s = s * pf2{-co, -co};
+        const pf2 h = pcmul(q.pa * pf2{co, co}, q.pb);
+        const pf2 pre = {ht_half ? s.x : h.x, ht_half ? s.y : h.y};
+        const pf2 P = pcmul(pcmul(pre, q.xu), q.xv);
+        acc = pcmadd(acc, P, q.xw);
+        __builtin_amdgcn_sched_barrier(0);
     }
     return cmk(acc.x, acc.y);
 }
