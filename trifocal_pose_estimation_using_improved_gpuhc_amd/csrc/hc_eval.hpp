@@ -73,6 +73,15 @@ static_assert(SLOT_OFF_P + 8 * NPP < 65536, "p offsets must fit 16 bits");
 //  hxd[q][l]  (lane l): SlotLDS byte offsets its slots 2q (bits 0..15) and 2q+1 (bits 16..31) store to
 //  ht[j][r] (row r's j-th dH/dt / H term): .x = off(p[a]) | off(p[b]) << 16
 //                                      .y = off(x[u]) | off(x[v]) << 8 | off(x[w]) << 16 | (int8)coef << 24
+// (float)(int8_t)(w.y >> 16) in one SDWA convert (the compiler's form took a
+// v_alignbit first); the dH/dt | H coefficient is the top byte.  (Float
+// coefficients in 12-byte term words measured no faster: profiles/r3p_*.)
+__device__ __forceinline__ float coef_hx(const uint2 &w) {
+    float co;
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(co) : "v"(w.y));
+    return co;
+}
+__device__ __forceinline__ float coef_ht(const uint2 &w) { return (float)((int)w.y >> 24); }
 struct EvalTables {
     int hx_len;
     int status;
@@ -82,6 +91,8 @@ struct EvalTables {
     unsigned long long pad2;
     uint32_t map[3][32];
     uint32_t hxd[HX_NSLOT / 2][32];
+    uint32_t ht_acc_mask[4];          // eval_rhs: lanes (of a half) that accumulate in help term q
+    uint32_t ht_light_mask[4];        // eval_rhs: lanes that accumulate a helper's product in light term q
     uint2 hx[HX_SLOT_CAP * 32];
     uint2 ht[HT_TERMS * 32];
 };
@@ -124,14 +135,16 @@ constexpr int EV_AHEAD = 2;
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
 struct HxOps { pf2 pa, pb, xu, xv; };
-__device__ __forceinline__ HxOps hx_ops(const char *sb, uint2 w) {
+template <typename TW>
+__device__ __forceinline__ HxOps hx_ops(const char *sb, const TW &w) {
     return HxOps{ldp(sb, w.x & 0xFFFFu), ldp(sb, w.x >> 16), ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu)};
 }
 
 // the term loop of eval_hx: operands are read through sb (x, p of the slot),
 // each finished entry is stored at sb + the lane's destination offset
-__device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const uint32_t *s_hxd, char *sb, int r) {
-    uint2 w[HX_SLOT_CAP];
+template <typename TW>
+__device__ __forceinline__ void eval_hx_terms(const TW *s_hx, const uint32_t *s_hxd, char *sb, int r) {
+    TW w[HX_SLOT_CAP];
     uint32_t dst[HX_NSLOT / 2];
 #pragma unroll
     for (int q = 0; q < HX_NSLOT / 2; q++) dst[q] = s_hxd[q * 32 + r];
@@ -146,11 +159,7 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const uint32_t 
         if (k + EV_WAHEAD < HX_SLOT_CAP) w[k + EV_WAHEAD] = s_hx[(k + EV_WAHEAD) * 32 + r];
         if (k + EV_AHEAD < HX_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
         const HxOps &q = o[k % (EV_AHEAD + 1)];
-        // (float)(int8_t)(w.y >> 16) in one SDWA convert (the compiler's form
-        // took a v_alignbit first)
-        float co;
-        asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2"
-            : "=v"(co) : "v"(w[k].y));
+        const float co = coef_hx(w[k]);
         pf2 P = q.pa * pf2{co, co};
         P = pcmul(P, q.pb);
         P = pcmul(P, q.xu);
@@ -171,126 +180,191 @@ __device__ __forceinline__ void eval_hx_terms(const uint2 *s_hx, const uint32_t 
 // where its group of terms ends, slot 6 (structural zero) is zeroed, and 30
 // gathers through the column -> slot map rebuild the register row.
 // the register row r of dH/dx from the lane's entry block (S.ent row r)
-__device__ __forceinline__ void gather_hx(cf (&rA)[NV], const uint32_t (&map)[3], const SlotLDS &S, int r) {
-    const cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
-    // opaque copy: keeps LICM from hoisting the 30 decoded gather addresses out
-    // of the path loop (30 VGPRs held across the LU, then spilled)
-    uint32_t m[3] = {map[0], map[1], map[2]};
-    asm volatile("" : "+v"(m[0]), "+v"(m[1]), "+v"(m[2]));
-    // slot = v_bfe_u32, address = v_lshl_add_u32 (2 VALU per column, not 3)
-    const char *eb = reinterpret_cast<const char *>(ent_row);
+// The gather map of row r: half c % 2 of word c / 2 = the SlotLDS byte
+// offset of column c's entry (its entry slot in row r's block of
+// SlotLDS::ent; slot 6: the structural zero), so a gather address is one
+// SDWA add, as the evaluations' operand addresses (a 3-bit slot code took a
+// v_bfe and a v_lshl_add).  Built once per launch; its 15 words are read from
+// LDS (stride 32 words) where the gather runs.
+constexpr int GM_WORDS = NV / 2;
+__device__ __forceinline__ uint32_t gather_map_word(const uint32_t (&map)[3], int r, int q) {
+    uint32_t v = 0;
+    for (int k = 0; k < 2; k++) {
+        const int c = 2 * q + k;
+        const uint32_t code = (map[c / 10] >> (3 * (c % 10))) & 7u;
+        v |= ((uint32_t)SLOT_OFF_ENT + 8u * ((uint32_t)(r < NV ? r : 0) * 7u + code)) << (16 * k);
+    }
+    return v;
+}
+__device__ __forceinline__ void gather_hx(cf (&rA)[NV], const uint32_t *gmw, const SlotLDS &S, int r) {
+    const char *sb = reinterpret_cast<const char *>(&S);
+    uint32_t g[GM_WORDS];
+#pragma unroll
+    for (int q = 0; q < GM_WORDS; q++) g[q] = gmw[q * 32 + r];
 #pragma unroll
     for (int c = 0; c < NV; c++) {
-        uint32_t code;   // asm: the compiler would turn bfe + shift back into shift + and + add
-        asm("v_bfe_u32 %0, %1, %2, 3" : "=v"(code) : "v"(m[c / 10]), "i"(3 * (c % 10)));
-        rA[c] = *reinterpret_cast<const cf *>(eb + (code << 3));
+        const pf2 v = ldp(sb, (c & 1) ? (g[c / 2] >> 16) : (g[c / 2] & 0xFFFFu));
+        rA[c] = cmk(v.x, v.y);
     }
 }
 
-__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint2 *s_hx, const uint32_t *s_hxd,
-                                        const uint32_t (&map)[3], SlotLDS &S, int r) {
+template <typename TW>
+__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const TW *s_hx, const uint32_t *s_hxd,
+                                        const uint32_t *gmw, SlotLDS &S, int r) {
     cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
     eval_hx_terms(s_hx, s_hxd, reinterpret_cast<char *>(&S), r);
     float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
     if (r < NV) ent_row[6] = cmk(z, z);   // structural zero
     wave_lds_sync();
-    gather_hx(rA, map, S, r);
+    gather_hx(rA, gmw, S, r);
 }
 
 struct HtOps { pf2 pa, pb, da, db, xu, xv, xw; };
-__device__ __forceinline__ HtOps ht_ops(const char *sb, uint2 w) {
+template <typename TW>
+__device__ __forceinline__ HtOps ht_ops(const char *sb, const TW &w) {
     const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
     return HtOps{ldp(sb, oa), ldp(sb, ob), ldp(sb + SLOT_DIF_DELTA, oa), ldp(sb + SLOT_DIF_DELTA, ob),
                  ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu), ldp(sb, (w.y >> 16) & 0xFFu)};
 }
 
-// dH/dt: b = -sum_j c*(d[a]*p[b] + d[b]*p[a])*x[u]*x[v]*x[w]
-__device__ __forceinline__ cf eval_ht(const uint2 *s_ht, const SlotLDS &S, int r) {
+// dH/dt, H and the merged pass share one loop (eval_rhs).
+//  * dH/dt: b = -sum_j c*(d[a]*p[b] + d[b]*p[a])*x[u]*x[v]*x[w]  (:91-119)
+//  * H:     b =  sum_j c*p[a]*p[b]*x[u]*x[v]*x[w]               (:122-148)
+//  * merged (RHS_MIXED): dH/dt in the halves with ht_half, H in the others, in
+//    one pass, for a wave whose two paths run different stage kinds
+//    (predictor | corrector: 44 % of the wave-stages of config 2) instead of
+//    both loops.  A term's x part ((prefix * x[u]) * x[v], accumulated with
+//    x[w]) is the same in both; the prefix is per half: dH/dt's
+//    -(c * (d[a]*p[b] + d[b]*p[a])), negated so that both accumulate acc +
+//    P*x[w] (acc - P*x[w] == acc + (-P)*x[w] bit for bit, and the negation
+//    passes through the products exactly), or H's (c * p[a]) * p[b].
+//
+// Balanced rows.  A row's terms form one sequential chain, and the rows of
+// this problem have 10 (rows 0..17), 13 or 16 terms, so a loop over the
+// longest row left most lanes idle for 6 terms.  The loop now runs
+// HT_FULL = 13 full terms and HT_HELP = 3 "light" ones: a row with 14..16
+// terms (an owner, lanes 16..29 of the half) computes its first 13 terms
+// itself; the products P of its last terms (everything but the accumulation
+// with x[w]) are computed by its partner lane (lane - 16, a row of at most 10
+// terms: a helper) in the helper's full terms 10 + q, and handed over with
+// one v_permlane16_swap per dword (lane i <-> i + 16, no LDS); the owner then
+// accumulates them, in order, in its light terms (one x[w] read each).  Lanes
+// mask the accumulation they must not do (k_prep_tables' masks: helpers in
+// their help terms, everyone but owners in the light terms).  Bit-exact: the
+// owner's chain is the same sequence of operations on the same values.
+enum : int { RHS_HT = 0, RHS_H = 1, RHS_MIXED = 2 };
+constexpr int HT_FULL = 13, HT_HELP = HT_TERMS - HT_FULL;
+constexpr int HT_HELP_FIRST = HT_FULL - HT_HELP;   // the helpers' own terms end here
+
+// acc +/- a*b in the lanes of m only (exec-masked packed fma pair, pcmadd /
+// pcmsub operation for operation; the other lanes keep acc)
+template <bool SUB>
+__device__ __forceinline__ pf2 pcmacc_masked(pf2 acc, pf2 a, pf2 b, unsigned long long m) {
+    pf2 t;
+    unsigned long long sv;
+    if constexpr (SUB)
+        asm("s_mov_b64 %2, exec\n\ts_mov_b64 exec, %3\n\t"
+            "v_pk_fma_f32 %1, %4, %5, %0 op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,0]\n\t"
+            "s_nop 0\n\t"
+            "v_pk_fma_f32 %0, %4, %5, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_hi:[1,0,0]\n\t"
+            "s_mov_b64 exec, %2"
+            : "+v"(acc), "=&v"(t), "=&s"(sv) : "s"(m), "v"(a), "v"(b));
+    else
+        asm("s_mov_b64 %2, exec\n\ts_mov_b64 exec, %3\n\t"
+            "v_pk_fma_f32 %1, %4, %5, %0 op_sel_hi:[0,1,1]\n\t"
+            "s_nop 0\n\t"
+            "v_pk_fma_f32 %0, %4, %5, %1 op_sel:[1,1,0] op_sel_hi:[1,0,1] neg_lo:[1,0,0]\n\t"
+            "s_mov_b64 exec, %2"
+            : "+v"(acc), "=&v"(t), "=&s"(sv) : "s"(m), "v"(a), "v"(b));
+    return acc;
+}
+// the helper's value of lane i reaches owner lane i + 16 (odd rows of 16
+// receive the even rows' values)
+__device__ __forceinline__ pf2 from_helper(pf2 v) {
+    const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.x), __float_as_uint(v.x), false, false);
+    const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.y), __float_as_uint(v.y), false, false);
+    return pf2{__uint_as_float(sx[0]), __uint_as_float(sy[0])};
+}
+struct RhsMasks { unsigned long long acc[HT_HELP], light[HT_HELP]; };
+
+__device__ __forceinline__ RhsMasks rhs_masks(const EvalTables *T) {
+    RhsMasks m;
+#pragma unroll
+    for (int q = 0; q < HT_HELP; q++) {
+        // uniform by construction; readfirstlane tells the compiler (SGPR operands)
+        const unsigned long long a = (uint32_t)__builtin_amdgcn_readfirstlane((int)T->ht_acc_mask[q]),
+                                 l = (uint32_t)__builtin_amdgcn_readfirstlane((int)T->ht_light_mask[q]);
+        m.acc[q] = a | (a << 32);
+        m.light[q] = l | (l << 32);
+    }
+    return m;
+}
+
+template <int KIND>
+struct RhsOps { pf2 pa, pb, da, db, xu, xv, xw; };
+template <int KIND, typename TW>
+__device__ __forceinline__ RhsOps<KIND> rhs_ops(const char *sb, const TW &w) {
+    const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
+    RhsOps<KIND> o;
+    o.pa = ldp(sb, oa);
+    o.pb = ldp(sb, ob);
+    if constexpr (KIND != RHS_H) {
+        o.da = ldp(sb + SLOT_DIF_DELTA, oa);
+        o.db = ldp(sb + SLOT_DIF_DELTA, ob);
+    }
+    o.xu = ldp(sb, w.y & 0xFFu);
+    o.xv = ldp(sb, (w.y >> 8) & 0xFFu);
+    o.xw = ldp(sb, (w.y >> 16) & 0xFFu);
+    return o;
+}
+
+template <int KIND, typename TW>
+__device__ __forceinline__ cf eval_rhs(const TW *s_ht, const SlotLDS &S, int r, bool ht_half, const RhsMasks &mk) {
     const char *sb = reinterpret_cast<const char *>(&S);
-    uint2 w[HT_TERMS];
+    constexpr bool SUB = KIND == RHS_HT;
+    TW w[HT_TERMS];
 #pragma unroll
     for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht[j * 32 + r];
-    HtOps o[EV_AHEAD + 1];
+    RhsOps<KIND> o[EV_AHEAD + 1];
 #pragma unroll
-    for (int j = 0; j < EV_AHEAD; j++) o[j] = ht_ops(sb, w[j]);
+    for (int j = 0; j < EV_AHEAD; j++) o[j] = rhs_ops<KIND>(sb, w[j]);
     pf2 acc = {0.0f, 0.0f};
+    pf2 hp[HT_HELP];
 #pragma unroll
-    for (int j = 0; j < HT_TERMS; j++) {
+    for (int j = 0; j < HT_FULL; j++) {
         if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht[(j + EV_WAHEAD) * 32 + r];
-        if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = ht_ops(sb, w[j + EV_AHEAD]);
-        const HtOps &q = o[j % (EV_AHEAD + 1)];
-        const float co = (float)((int)w[j].y >> 24);
-        pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
-        s = s * pf2{co, co};
-        const pf2 P = pcmul(pcmul(s, q.xu), q.xv);
-        acc = pcmsub(acc, P, q.xw);
+        if (j + EV_AHEAD < HT_FULL) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = rhs_ops<KIND>(sb, w[j + EV_AHEAD]);
+        const RhsOps<KIND> &q = o[j % (EV_AHEAD + 1)];
+        const float co = coef_ht(w[j]);
+        pf2 P;
+        if constexpr (KIND == RHS_HT) {
+            pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
+            s = s * pf2{co, co};
+            P = pcmul(pcmul(s, q.xu), q.xv);
+        } else if constexpr (KIND == RHS_H) {
+            P = q.pa * pf2{co, co};
+            P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
+        } else {
+            pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
+            s = s * pf2{-co, -co};
+            const pf2 h = pcmul(q.pa * pf2{co, co}, q.pb);
+            const pf2 pre = {ht_half ? s.x : h.x, ht_half ? s.y : h.y};
+            P = pcmul(pcmul(pre, q.xu), q.xv);
+        }
+        if (j < HT_HELP_FIRST) {
+            acc = SUB ? pcmsub(acc, P, q.xw) : pcmadd(acc, P, q.xw);
+        } else {   // helpers compute a partner's product here instead of accumulating
+            hp[j - HT_HELP_FIRST] = P;
+            acc = pcmacc_masked<SUB>(acc, P, q.xw, mk.acc[j - HT_HELP_FIRST]);
+        }
         __builtin_amdgcn_sched_barrier(0);   // keep the look-ahead reads ahead (no sinking to their uses)
     }
-    return cmk(acc.x, acc.y);
-}
-
-// dH/dt in the halves with ht_half, H in the others, in one pass: for a wave
-// whose two paths run different stage kinds (predictor | corrector: 44 % of
-// the wave-stages of config 2), instead of both full loops.  A term's x part
-// ((prefix * x[u]) * x[v], accumulated with x[w]) is the same in both; the
-// prefix is per half:
-//   dH/dt: -(c * (d[a]*p[b] + d[b]*p[a])), negated so that the accumulation
-//          is acc + P*x[w] in both (acc - P*x[w] == acc + (-P)*x[w] bit for
-//          bit, and the negation passes through the products exactly);
-//   H:     (c * p[a]) * p[b].
-__device__ __forceinline__ cf eval_hth(const uint2 *s_ht, const SlotLDS &S, int r, bool ht_half) {
-    const char *sb = reinterpret_cast<const char *>(&S);
-    uint2 w[HT_TERMS];
 #pragma unroll
-    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht[j * 32 + r];
-    HtOps o[EV_AHEAD + 1];
-#pragma unroll
-    for (int j = 0; j < EV_AHEAD; j++) o[j] = ht_ops(sb, w[j]);
-    pf2 acc = {0.0f, 0.0f};
-#pragma unroll
-    for (int j = 0; j < HT_TERMS; j++) {
-        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht[(j + EV_WAHEAD) * 32 + r];
-        if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = ht_ops(sb, w[j + EV_AHEAD]);
-        const HtOps &q = o[j % (EV_AHEAD + 1)];
-        const float co = (float)((int)w[j].y >> 24);
-        pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
-        s = s * pf2{-co, -co};
-        const pf2 h = pcmul(q.pa * pf2{co, co}, q.pb);
-        const pf2 pre = {ht_half ? s.x : h.x, ht_half ? s.y : h.y};
-        const pf2 P = pcmul(pcmul(pre, q.xu), q.xv);
-        acc = pcmadd(acc, P, q.xw);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    return cmk(acc.x, acc.y);
-}
-
-struct HOps { pf2 pa, pb, xu, xv, xw; };
-__device__ __forceinline__ HOps h_ops(const char *sb, uint2 w) {
-    return HOps{ldp(sb, w.x & 0xFFFFu), ldp(sb, w.x >> 16), ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu),
-                ldp(sb, (w.y >> 16) & 0xFFu)};
-}
-
-// H: b = sum_j c*p[a]*p[b]*x[u]*x[v]*x[w]
-__device__ __forceinline__ cf eval_h(const uint2 *s_ht, const SlotLDS &S, int r) {
-    const char *sb = reinterpret_cast<const char *>(&S);
-    uint2 w[HT_TERMS];
-#pragma unroll
-    for (int j = 0; j < EV_WAHEAD; j++) w[j] = s_ht[j * 32 + r];
-    HOps o[EV_AHEAD + 1];
-#pragma unroll
-    for (int j = 0; j < EV_AHEAD; j++) o[j] = h_ops(sb, w[j]);
-    pf2 acc = {0.0f, 0.0f};
-#pragma unroll
-    for (int j = 0; j < HT_TERMS; j++) {
-        if (j + EV_WAHEAD < HT_TERMS) w[j + EV_WAHEAD] = s_ht[(j + EV_WAHEAD) * 32 + r];
-        if (j + EV_AHEAD < HT_TERMS) o[(j + EV_AHEAD) % (EV_AHEAD + 1)] = h_ops(sb, w[j + EV_AHEAD]);
-        const HOps &q = o[j % (EV_AHEAD + 1)];
-        const float co = (float)((int)w[j].y >> 24);
-        pf2 P = q.pa * pf2{co, co};
-        P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
-        acc = pcmadd(acc, P, q.xw);
-        __builtin_amdgcn_sched_barrier(0);
+    for (int q = 0; q < HT_HELP; q++) {     // owners: the partner's products, in order
+        const pf2 P = from_helper(hp[q]);
+        const pf2 xw = ldp(sb, (w[HT_FULL + q].y >> 16) & 0xFFu);
+        acc = pcmacc_masked<SUB>(acc, P, xw, mk.light[q]);
     }
     return cmk(acc.x, acc.y);
 }

@@ -343,6 +343,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
     // row, then lower column), numbering each row's entries 0..5 in placement
     // order; C: rows write their entries' term words at their places.
     __shared__ uint8_t s_cnt[NV][NV];
+    __shared__ int s_htn[32];             // dH/dt | H terms of row r (0 for lanes 30, 31)
     __shared__ uint8_t s_place[NV][NV];   // lane << 3 | slot, 0xFF: structural zero
     __shared__ uint32_t s_map[3][32];
     __shared__ uint32_t s_dst[HX_NSLOT / 2][32];
@@ -363,8 +364,14 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
             s_cnt[r][c] = (uint8_t)n;
             s_place[r][c] = 0xFFu;
         }
-    if (r < 32)
+    if (r < 32) {
         for (int k2 = 0; k2 < HX_SLOT_CAP; k2++) T->hx[k2 * 32 + r] = pad_hx;
+        int n = 0;
+        if (r < NV)
+            for (int j = 0; j < HT_TERMS; j++)
+                if (U[HX_SIZE + j * HT_PARTS * NV + r] != 0) n++;
+        s_htn[r] = n;
+    }
     __syncthreads();
     if (tid == 0) {
         int used[HX_NSLOT], order[HX_NSLOT], ne[NV];
@@ -425,7 +432,17 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                 }
             }
         s_len[r] = HX_SLOT_CAP;
+        // dH/dt | H (hc_eval.hpp eval_rhs): own terms at positions 0..12; a row
+        // of more than 13 terms (an owner, lanes 16..29) puts its terms 14.. in
+        // its light words 13.. (for x[w]) and in its helper's (lane - 16)
+        // words 10..; the helper's own terms must end before 10
         const int32_t *D = U + HX_SIZE;
+        const int n = s_htn[r];
+        const int need_o = max(0, n - HT_FULL);
+        const int need_h = r < 16 ? max(0, s_htn[r + 16] - HT_FULL) : 0;
+        if (need_o > 0 && (r < 16 || s_htn[r - 16] > HT_HELP_FIRST)) bad = true;
+        if (need_h > 0 && n > HT_HELP_FIRST) bad = true;
+        const uint2 pad_ht = make_uint2(pad_hx.x, pad_hx.y | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 16));
         int k = 0;
         if (r < NV) {
             for (int j = 0; j < HT_TERMS; j++) {
@@ -435,19 +452,32 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                 if (co == 0) continue;
                 bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
                        v < 0 || v > NV || x3 < 0 || x3 > NV;
-                if (!bad)
-                    T->ht[k * 32 + r] = make_uint2(
-                        (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
-                        (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
-                            ((uint32_t)(SLOT_OFF_X + 8 * x3) << 16) | (((uint32_t)co & 0xFFu) << 24));
+                const uint2 tw = make_uint2(
+                    (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
+                    (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
+                        ((uint32_t)(SLOT_OFF_X + 8 * x3) << 16) | (((uint32_t)co & 0xFFu) << 24));
+                if (!bad) {
+                    T->ht[k * 32 + r] = tw;   // k < 13: a full term; k >= 13: the light word (x[w])
+                    if (k >= HT_FULL) T->ht[(HT_HELP_FIRST + k - HT_FULL) * 32 + (r - 16)] = tw;
+                }
                 k++;
             }
         }
-        for (; k < HT_TERMS; k++) T->ht[k * 32 + r] = make_uint2(pad_hx.x, pad_hx.y | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 16));
+        for (int q = k; q < HT_TERMS; q++)
+            if (!(q >= HT_HELP_FIRST && q < HT_HELP_FIRST + need_h)) T->ht[q * 32 + r] = pad_ht;
         if (bad) atomicOr(&s_bad, 1);
     }
     __syncthreads();
     if (r == 0) {
+        // eval_rhs masks: help term q of the helpers (no accumulation), light
+        // term q of the owners
+        for (int q = 0; q < 4; q++) {
+            uint32_t am = 0xFFFFFFFFu, lm = 0u;
+            for (int l = 16; l < 32; l++)
+                if (s_htn[l] - HT_FULL > q) { am &= ~(1u << (l - 16)); lm |= 1u << l; }
+            T->ht_acc_mask[q] = am;
+            T->ht_light_mask[q] = lm;
+        }
         int mx = 0;
         for (int q = 0; q < 32; q++) mx = max(mx, s_len[q]);
         T->hx_len = mx;
@@ -569,13 +599,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     if (r == 0) S.p[33] = cmk(1.0f, 0.0f);
     // per-row constants (column->slot maps, structural pattern) live in LDS and
     // are re-read every stage: held in VGPRs across the loop they spill (abort mode)
-    __shared__ uint32_t s_rowc[4][32];
+    __shared__ uint32_t s_rowc[GM_WORDS + 1][32];   // [0..14] gather map (hc_eval.hpp), [15] structural pattern
     if (threadIdx.x < 32) {
         const uint32_t m0[3] = {T->map[0][threadIdx.x], T->map[1][threadIdx.x], T->map[2][threadIdx.x]};
-        s_rowc[0][threadIdx.x] = m0[0];
-        s_rowc[1][threadIdx.x] = m0[1];
-        s_rowc[2][threadIdx.x] = m0[2];
-        s_rowc[3][threadIdx.x] = row_pattern(m0);   // structural pattern of row r
+        for (int q = 0; q < GM_WORDS; q++) s_rowc[q][threadIdx.x] = gather_map_word(m0, threadIdx.x, q);
+        s_rowc[GM_WORDS][threadIdx.x] = row_pattern(m0);   // structural pattern of row r
     }
     __syncthreads();
     const bool rl = r < NV;
@@ -920,8 +948,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         // constants (bpermute addresses, r == i masks) out of the path loop
         const int lane_v = lane_fresh();   // recomputed (2 VALU), not held across the loop
         const int r_v = lane_v & 31;
-        const uint32_t map[3] = {s_rowc[0][r_v], s_rowc[1][r_v], s_rowc[2][r_v]};
-        const uint32_t row_pat = s_rowc[3][r_v];
+        const uint32_t row_pat = s_rowc[GM_WORDS][r_v];
         const bool act = ph_in == PH_STAGE;
         const bool pred = act && s_in < 4;
         HC_DIAG_MARK(1);
@@ -931,19 +958,20 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         cf rB = cmk(0.0f, 0.0f);
         {
             const bool any_p = __ballot(pred) != 0ull, any_c = __ballot(act && !pred) != 0ull;
+            const RhsMasks mk = rhs_masks(T);
             if (any_p && any_c) {                                            // :185 | :221, one pass
-                rB = eval_hth(s_ht, S, r_v, pred);
+                rB = eval_rhs<RHS_MIXED>(s_ht, S, r_v, pred, mk);
             } else if (any_p) {                                              // :185
-                const cf t = eval_ht(s_ht, S, r_v);
+                const cf t = eval_rhs<RHS_HT>(s_ht, S, r_v, true, mk);
                 if (pred) rB = t;
             } else if (any_c) {                                              // :221
-                const cf t = eval_h(s_ht, S, r_v);
+                const cf t = eval_rhs<RHS_H>(s_ht, S, r_v, false, mk);
                 if (!pred) rB = t;
             }
         }
         HC_DIAG_MARK(3);
         cf rA[NV];
-        eval_hx(rA, s_hx, s_hxd, map, S, r_v);                               // :184 / :220
+        eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_v);                     // :184 / :220
         wave_lds_sync();
         HC_DIAG_MARK(2);
         bool redo;
@@ -963,14 +991,14 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             const bool act_r = S.st.ph == PH_STAGE, pred_r = act_r && S.st.s < 4;
             cf rb = cmk(0.0f, 0.0f);
             if (__ballot(pred_r) != 0ull) {
-                const cf t = eval_ht(s_ht, S, r_v);
+                const cf t = eval_rhs<RHS_HT>(s_ht, S, r_v, true, rhs_masks(T));
                 if (pred_r) rb = t;
             }
             if (__ballot(act_r && !pred_r) != 0ull) {
-                const cf t = eval_h(s_ht, S, r_v);
+                const cf t = eval_rhs<RHS_H>(s_ht, S, r_v, false, rhs_masks(T));
                 if (!pred_r) rb = t;
             }
-            gather_hx(rA, map, S, r_v);
+            gather_hx(rA, &s_rowc[0][0], S, r_v);
 #ifdef HC_DIAG_LUWORK
             k = lu_solve<true>(rA, rb, lane_v, row_pat, LB, redo, __ballot(act_r));
 #else
@@ -1132,12 +1160,17 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
         S.dif[r] = D[(size_t)sys * NPP + r];
         if (r < NPP - 32) { S.p[r + 32] = P[(size_t)sys * NPP + r + 32]; S.dif[r + 32] = D[(size_t)sys * NPP + r + 32]; }
     }
-    const uint32_t map[3] = {T->map[0][r], T->map[1][r], T->map[2][r]};
+    __shared__ uint32_t s_gm[GM_WORDS][32];
+    if (threadIdx.x < 32) {
+        const uint32_t m0[3] = {T->map[0][threadIdx.x], T->map[1][threadIdx.x], T->map[2][threadIdx.x]};
+        for (int q = 0; q < GM_WORDS; q++) s_gm[q][threadIdx.x] = gather_map_word(m0, threadIdx.x, q);
+    }
+    __syncthreads();
     wave_lds_sync();
     cf rA[NV];
-    eval_hx(rA, s_hx, s_hxd, map, S, r);
-    const cf ht = eval_ht(s_ht, S, r);
-    const cf h = eval_h(s_ht, S, r);
+    eval_hx(rA, s_hx, s_hxd, &s_gm[0][0], S, r);
+    const cf ht = eval_rhs<RHS_HT>(s_ht, S, r, true, rhs_masks(T));
+    const cf h = eval_rhs<RHS_H>(s_ht, S, r, false, rhs_masks(T));
     if (ok && r < NV) {
 #pragma unroll
         for (int c = 0; c < NV; c++) HX[((size_t)sys * NV + r) * NV + c] = rA[c];
