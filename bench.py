@@ -40,11 +40,29 @@ FLOP_CORR_STAGE = 101.3e3    # Hx 12,276 + H 10,080 + LU 78,670 + update/norms ~
 # The LU's rank-1 updates are 8555 element updates (8 FLOP each = 68,440 FLOP)
 # of the 78,670 in the dense algorithm the reference runs.  The structurally
 # sparse LU executes only the column groups that are non-zero in a pivot row
-# of the wave: 5,040.1 elements per solve on config 2 (0.589 of dense), measured
-# by the HC_DIAG_LUWORK build (scripts/lu_work.py, profiles/r3j_lu_work.json).
+# of the wave (0.589 of dense with groups of 4 columns, round 3 first half), measured
+# by the HC_DIAG_LUWORK build (scripts/lu_work.py, profiles/*_lu_work.json; read
+# by lu_executed_fraction, since it depends on the LU's column-group size).
 LU_UPDATE_DENSE_FLOP = 68440.0
-LU_UPDATE_EXECUTED_FRACTION = 0.5891
-LU_EXEC_SAVING = LU_UPDATE_DENSE_FLOP * (1.0 - LU_UPDATE_EXECUTED_FRACTION)
+
+
+def lu_executed_fraction():
+    """Executed fraction of the dense rank-1 update work, from the newest
+    committed config-2 HC_DIAG_LUWORK measurement of the kernel
+    (profiles/*_lu_work.json; the fraction depends on the LU's column-group
+    size): (fraction, file)."""
+    import glob
+    best = (0.5891, "profiles/r3j_lu_work.json")
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_lu_work.json"))):
+        if "scaled" in os.path.basename(f):
+            continue
+        try:
+            with open(f) as fh:
+                d = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
+            best = (float(d["executed_fraction"]), os.path.relpath(f, ROOT))
+        except (OSError, ValueError, KeyError, IndexError):
+            continue
+    return best
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak (64 FLOP/clk/SIMD) == FP32 MFMA peak
 HBM_PEAK_GBS = 8000.0
 TRACK_KERNEL = "void hc::k_track<false, 5, true, false>(hc::KArgs)"
@@ -223,7 +241,8 @@ def main():
     steps_sum = int(host["stats"]["steps"].astype(np.int64).sum())
     corr_sum = int(host["stats"]["corrections"].astype(np.int64).sum())
     flops = steps_sum * 4 * FLOP_PRED_STAGE + corr_sum * FLOP_CORR_STAGE          # dense-LU convention
-    flops_exec = flops - (steps_sum * 4 + corr_sum) * LU_EXEC_SAVING               # LU updates as executed
+    lu_frac, lu_frac_src = lu_executed_fraction()
+    flops_exec = flops - (steps_sum * 4 + corr_sum) * LU_UPDATE_DENSE_FLOP * (1.0 - lu_frac)   # LU updates as executed
     from trifocal_pose_estimation_using_improved_gpuhc_amd import count_solutions
     counts = count_solutions(host["tracks"], host["converge"], host["infinity"])
 
@@ -354,10 +373,12 @@ def main():
                                  "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = FLOPs of "
                                  "the executed stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 kFLOP / "
                                  "corrector stage, with the LU's rank-1 updates counted over the column groups "
-                                 "the structurally sparse LU executes: 0.589 of the dense 68.4 kFLOP, "
-                                 "profiles/r3j_lu_work.json) / median single-launch kernel time (HIP events on "
-                                 "the launch stream). achieved_dense_lu prices the LU as the reference's dense "
-                                 "algorithm.",
+                                 "the structurally sparse LU executes: lu_executed_fraction of the dense 68.4 "
+                                 "kFLOP, measured by the HC_DIAG_LUWORK build in lu_executed_fraction_source) / "
+                                 "median single-launch kernel time (HIP events on the launch stream). "
+                                 "achieved_dense_lu prices the LU as the reference's dense algorithm.",
+                         "lu_executed_fraction": round(lu_frac, 4),
+                         "lu_executed_fraction_source": lu_frac_src,
                          "kernel_ms": round(float(np.median(launch_ms)), 4),
                          "executed_gflop_per_launch": round(flops_exec / 1e9, 3),
                          "dense_lu_gflop_per_launch": round(flops / 1e9, 3),

@@ -193,7 +193,13 @@ hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspa
 /* Device-side outcome of the last launch on this workspace:
      HC_SUCCESS;
      HC_ERROR_TABLE  -- the index table does not fit the kernels' compaction
-                        (the tracker then left every output untouched);
+                        (the tracker then left every output untouched): an
+                        index or coefficient out of range, dH/dx entries that
+                        do not bin-pack into the 32 lanes' entry slots of
+                        8, 5, 3, 3, 1, 1 terms (or a row of more than 6
+                        entries), or a dH/dt | H row of more than 13 terms
+                        whose partner row (lane ^ 16) has more than 10
+                        (Evaluations);
      HC_ERROR_DEVICE -- time slicing only: a suspended path could not be handed
                         over (its ring entry never arrived within the bounded
                         wait, or the ring overflowed); that path's converge /

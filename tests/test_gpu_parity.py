@@ -420,3 +420,67 @@ def test_ph_matches_golden_N100(problem, samples100, tracker):
     assert (r["stats"]["steps"] == g["steps"]).all()
     assert (r["stats"]["corrections"] == g["corrections"]).all()
     assert (track_hash(r["tracks"]) == g["hash"]).all()
+
+
+def _row_permuted(problem, perm):
+    """The index tables with the equations (rows) reordered: row r of the new
+    system is row perm[r] of the reference's (a valid, equivalent problem)."""
+    dx = problem.dHdx_index.reshape(-1, 30)[:, perm].reshape(-1)
+    dt = problem.dHdt_index.reshape(-1, 30)[:, perm].reshape(-1)
+    return (np.ascontiguousarray(dx, np.int32), np.ascontiguousarray(dt, np.int32),
+            np.ascontiguousarray(np.concatenate([dx, dt]), np.int32))
+
+
+def test_eval_row_permuted_tables_match_oracle(problem, oracle, samples100):
+    """The table builder's lane assignments (dH/dx entries bin-packed over the
+    32 lanes, the dH/dt | H owner / helper pairs lane ^ 16) for equation orders
+    other than the reference's: reversed (the long dH/dt rows land in lanes
+    0..11, their helpers in 16..27) and a random order that still pairs every
+    long row with a short one."""
+    from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import eval_batched
+    tgt, dif, _ = samples100
+    X, P, D = _jacobians_from_path(problem, oracle, tgt, dif, n=48, seed=5)
+    nt = (problem.dHdt_index.reshape(-1, 30)[::6] != 0).sum(axis=0)   # terms per row (coefficient rows)
+    rng = np.random.default_rng(11)
+    perms = [np.arange(29, -1, -1)]
+    while len(perms) < 2:
+        p = rng.permutation(30)
+        n = nt[p]
+        if all(not (n[r] > 13 and (r ^ 16 >= 30 or n[r ^ 16] > 10)) for r in range(30)):
+            perms.append(p)
+    for perm in perms:
+        dx, dt, U = _row_permuted(problem, perm)
+        HX, HT, H = eval_batched(U, X, P, D)
+        for i in range(X.shape[0]):
+            assert same(HX[i], oracle.eval_hx(dx, X[i], P[i])).all(), f"dH/dx mismatch at point {i}, perm {perm}"
+            assert same(HT[i], oracle.eval_ht(dt, X[i], P[i], D[i])).all(), f"dH/dt mismatch {i}, perm {perm}"
+            assert same(H[i], oracle.eval_h(dt, X[i], P[i])).all(), f"H mismatch {i}, perm {perm}"
+
+
+def test_eval_rejects_tables_without_helpers(problem):
+    """Two long dH/dt rows paired as lane ^ 16 partners (neither can help the
+    other): the table builder rejects the table (HC_ERROR_TABLE) and the
+    kernels leave their outputs untouched."""
+    import ctypes as C
+    import torch
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+    perm = np.arange(30)
+    perm[2], perm[19] = 19, 2          # lanes 2 and 18: rows 19 and 18, 16 terms each
+    _, _, U = _row_permuted(problem, perm)
+    L = _abi.lib()
+    dev = torch.device("cuda:0")
+    n = 4
+    Ut = torch.from_numpy(U).to(dev)
+    X = torch.zeros((n, 31, 2), dtype=torch.float32, device=dev)
+    P = torch.zeros((n, 34, 2), dtype=torch.float32, device=dev)
+    HX = torch.full((n, 30, 30, 2), 7.0, dtype=torch.float32, device=dev)
+    HT = torch.full((n, 30, 2), 7.0, dtype=torch.float32, device=dev)
+    H = torch.full((n, 30, 2), 7.0, dtype=torch.float32, device=dev)
+    wsb = int(L.hc_trifocal_workspace_size())
+    ws = torch.zeros(wsb, dtype=torch.uint8, device=dev)
+    p = lambda t: C.c_void_p(t.data_ptr())  # noqa: E731
+    _abi.check(L.hc_trifocal_eval_batched(n, p(Ut), p(X), p(P), p(P), p(HX), p(HT), p(H), p(ws), wsb,
+                                          C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)), "eval")
+    torch.cuda.synchronize(dev)
+    assert int(L.hc_trifocal_workspace_status(p(ws))) == 5   # HC_ERROR_TABLE
+    assert (HX == 7.0).all() and (HT == 7.0).all() and (H == 7.0).all()

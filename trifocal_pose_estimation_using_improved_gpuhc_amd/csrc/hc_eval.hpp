@@ -244,11 +244,11 @@ __device__ __forceinline__ HtOps ht_ops(const char *sb, const TW &w) {
 // this problem have 10 (rows 0..17), 13 or 16 terms, so a loop over the
 // longest row left most lanes idle for 6 terms.  The loop now runs
 // HT_FULL = 13 full terms and HT_HELP = 3 "light" ones: a row with 14..16
-// terms (an owner, lanes 16..29 of the half) computes its first 13 terms
-// itself; the products P of its last terms (everything but the accumulation
-// with x[w]) are computed by its partner lane (lane - 16, a row of at most 10
-// terms: a helper) in the helper's full terms 10 + q, and handed over with
-// one v_permlane16_swap per dword (lane i <-> i + 16, no LDS); the owner then
+// terms (an owner) computes its first 13 terms itself; the products P of its
+// last terms (everything but the accumulation with x[w]) are computed by its
+// partner lane (lane ^ 16, a row of at most 10 terms: a helper) in the
+// helper's full terms 10 + q, and handed over with one v_permlane16_swap per
+// dword (lane i <-> i ^ 16, no LDS); the owner then
 // accumulates them, in order, in its light terms (one x[w] read each).  Lanes
 // mask the accumulation they must not do (k_prep_tables' masks: helpers in
 // their help terms, everyone but owners in the light terms).  Bit-exact: the
@@ -279,12 +279,12 @@ __device__ __forceinline__ pf2 pcmacc_masked(pf2 acc, pf2 a, pf2 b, unsigned lon
             : "+v"(acc), "=&v"(t), "=&s"(sv) : "s"(m), "v"(a), "v"(b));
     return acc;
 }
-// the helper's value of lane i reaches owner lane i + 16 (odd rows of 16
-// receive the even rows' values)
-__device__ __forceinline__ pf2 from_helper(pf2 v) {
-    const auto sx = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.x), __float_as_uint(v.x), false, false);
-    const auto sy = __builtin_amdgcn_permlane16_swap(__float_as_uint(v.y), __float_as_uint(v.y), false, false);
-    return pf2{__uint_as_float(sx[0]), __uint_as_float(sy[0])};
+// the partner's value: lane i <-> lane i ^ 16 within each half (rows of 16
+// lanes swapped in pairs: v_permlane16_swap with one register as both
+// operands, one VALU per dword and no copy)
+__device__ __forceinline__ pf2 from_partner(pf2 v) {
+    asm("v_permlane16_swap_b32 %0, %0\n\tv_permlane16_swap_b32 %1, %1" : "+v"(v.x), "+v"(v.y));
+    return v;
 }
 struct RhsMasks { unsigned long long acc[HT_HELP], light[HT_HELP]; };
 
@@ -362,7 +362,7 @@ __device__ __forceinline__ cf eval_rhs(const TW *s_ht, const SlotLDS &S, int r, 
     }
 #pragma unroll
     for (int q = 0; q < HT_HELP; q++) {     // owners: the partner's products, in order
-        const pf2 P = from_helper(hp[q]);
+        const pf2 P = from_partner(hp[q]);
         const pf2 xw = ldp(sb, (w[HT_FULL + q].y >> 16) & 0xFFu);
         acc = pcmacc_masked<SUB>(acc, P, xw, mk.light[q]);
     }

@@ -433,14 +433,14 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
             }
         s_len[r] = HX_SLOT_CAP;
         // dH/dt | H (hc_eval.hpp eval_rhs): own terms at positions 0..12; a row
-        // of more than 13 terms (an owner, lanes 16..29) puts its terms 14.. in
-        // its light words 13.. (for x[w]) and in its helper's (lane - 16)
-        // words 10..; the helper's own terms must end before 10
+        // of more than 13 terms (an owner) puts its terms 14.. in its light
+        // words 13.. (for x[w]) and in its helper's (lane ^ 16) words 10..; the
+        // helper's own terms must end before 10 and it needs no help itself
         const int32_t *D = U + HX_SIZE;
         const int n = s_htn[r];
         const int need_o = max(0, n - HT_FULL);
-        const int need_h = r < 16 ? max(0, s_htn[r + 16] - HT_FULL) : 0;
-        if (need_o > 0 && (r < 16 || s_htn[r - 16] > HT_HELP_FIRST)) bad = true;
+        const int need_h = max(0, s_htn[r ^ 16] - HT_FULL);
+        if (need_o > 0 && s_htn[r ^ 16] > HT_HELP_FIRST) bad = true;
         if (need_h > 0 && n > HT_HELP_FIRST) bad = true;
         const uint2 pad_ht = make_uint2(pad_hx.x, pad_hx.y | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 16));
         int k = 0;
@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                         ((uint32_t)(SLOT_OFF_X + 8 * x3) << 16) | (((uint32_t)co & 0xFFu) << 24));
                 if (!bad) {
                     T->ht[k * 32 + r] = tw;   // k < 13: a full term; k >= 13: the light word (x[w])
-                    if (k >= HT_FULL) T->ht[(HT_HELP_FIRST + k - HT_FULL) * 32 + (r - 16)] = tw;
+                    if (k >= HT_FULL) T->ht[(HT_HELP_FIRST + k - HT_FULL) * 32 + (r ^ 16)] = tw;
                 }
                 k++;
             }
@@ -473,8 +473,8 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         // term q of the owners
         for (int q = 0; q < 4; q++) {
             uint32_t am = 0xFFFFFFFFu, lm = 0u;
-            for (int l = 16; l < 32; l++)
-                if (s_htn[l] - HT_FULL > q) { am &= ~(1u << (l - 16)); lm |= 1u << l; }
+            for (int l = 0; l < 32; l++)
+                if (s_htn[l] - HT_FULL > q) { am &= ~(1u << (l ^ 16)); lm |= 1u << l; }
             T->ht_acc_mask[q] = am;
             T->ht_light_mask[q] = lm;
         }
@@ -565,6 +565,7 @@ __device__ unsigned long long g_diag_phase[13];
 typedef uint32_t T_hxd_t[HX_NSLOT / 2][32];
 template <bool ABORT, int MINW, bool GTAB, bool ARCH = false>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
+    constexpr int LUCH = ABORT ? 4 : LU_CHUNK;   // LU column group (hc_lu.hpp): latency (abort) vs throughput
     constexpr int TAB_BYTES = GTAB ? 16 : (int)(sizeof(uint2) * (HX_SLOT_CAP + HT_TERMS) * 32 + sizeof(T_hxd_t));
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
@@ -977,9 +978,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         bool redo;
         LUBuf &LB = *reinterpret_cast<LUBuf *>(S.lu);
 #ifdef HC_DIAG_LUWORK
-        cf k = lu_solve<false>(rA, rB, lane_v, row_pat, LB, redo, __ballot(act));   // :188 / :224
+        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, redo, __ballot(act));   // :188 / :224
 #else
-        cf k = lu_solve<false>(rA, rB, lane_v, row_pat, LB, redo);                  // :188 / :224
+        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, redo);                  // :188 / :224
 #endif
         if (__builtin_expect(redo, 0)) {
             // a system the sparse solve cannot take exactly (an entry not provably
@@ -1000,9 +1001,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             }
             gather_hx(rA, &s_rowc[0][0], S, r_v);
 #ifdef HC_DIAG_LUWORK
-            k = lu_solve<true>(rA, rb, lane_v, row_pat, LB, redo, __ballot(act_r));
+            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, redo, __ballot(act_r));
 #else
-            k = lu_solve<true>(rA, rb, lane_v, row_pat, LB, redo);
+            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, redo);
 #endif
         }
         wave_lds_sync();

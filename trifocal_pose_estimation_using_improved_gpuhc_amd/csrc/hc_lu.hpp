@@ -62,7 +62,12 @@ struct alignas(16) LUBuf {
 static_assert(sizeof(LUBuf) == sizeof(SlotLDS::lu), "LUBuf is SlotLDS::lu");
 static_assert(offsetof(SlotLDS, lu) % 16 == 0, "SlotLDS::lu must be 16-B aligned");
 
-constexpr int LU_CHUNK = 4;   // columns per skippable group (even)
+// columns per skippable group (a template parameter CH below): 2 for the
+// tracking kernels, where the LDS stores of dead columns are what a wider group
+// costs (profiles/r3u_ab_oo_rz_gs_chunk2.jsonl: 33.55 -> 31.78 ms per config-2
+// launch), 4 for the abort kernel, whose time to the first pose is set by a
+// lone wave's latency (one group test per 4 columns; lone sample 11.2 vs 12.3 ms)
+constexpr int LU_CHUNK = 2;
 
 // Correctly rounded 1/s for s in [2^-90, 2^120): v_rcp_f32 plus one Newton
 // step (bit-identical to hipcc's div_scale / div_fmas / div_fixup sequence
@@ -97,6 +102,15 @@ __device__ __forceinline__ int half_max_int_p16(int v) {
     v = max(v, dpp_i<DPP_ROW_MIRROR>(v));
     const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
     return max((int)sw[0], (int)sw[1]);
+}
+
+__device__ __forceinline__ int half_min_int_p16(int v) {
+    v = min(v, dpp_i<DPP_QP_1032>(v));
+    v = min(v, dpp_i<DPP_QP_2301>(v));
+    v = min(v, dpp_i<DPP_ROW_HALF_MIRROR>(v));
+    v = min(v, dpp_i<DPP_ROW_MIRROR>(v));
+    const auto sw = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return min((int)sw[0], (int)sw[1]);
 }
 
 // structural pattern of row r from its column->entry-slot map (slot 6 = zero)
@@ -158,13 +172,16 @@ struct LuChunks {
 // Group tests on one bit: gbits = pmw | pmw >> 1 | pmw >> 2 | pmw >> 3, so bit J
 // says "some column of J..J+3 may be non-zero" and a group test is s_bitcmp1
 // + s_cbranch (the compiler keeps an s_cmp after a multi-bit s_and).
+template <int CH>
 __device__ __forceinline__ uint32_t group_bits(uint32_t pmw) {
-    const uint32_t t = pmw | (pmw >> 1);
-    return t | (t >> 2);
+    uint32_t t = pmw;
+#pragma unroll
+    for (int k = 1; k < CH; k++) t |= pmw >> k;
+    return t;
 }
-template <int I, int K>
+template <int I, int K, int CH>
 __device__ __forceinline__ bool group_live(uint32_t pmw, uint32_t gb) {
-    using C = LuChunks<LU_CHUNK>;
+    using C = LuChunks<CH>;
     constexpr int J = C::start(I, K), N = C::len(I, K);
     if constexpr (N == 1) return (pmw >> J) & 1u;
     else return (gb >> J) & 1u;
@@ -172,12 +189,12 @@ __device__ __forceinline__ bool group_live(uint32_t pmw, uint32_t gb) {
 
 // pivot lane: row elements of the groups of step I that are non-zero in some
 // pivot row of the wave
-template <int I, int K>
+template <int I, int K, int CH>
 __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uint32_t gb, LUBuf &L) {
-    using C = LuChunks<LU_CHUNK>;
+    using C = LuChunks<CH>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (__builtin_expect(group_live<I, K>(pmw, gb), 1)) {
+        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
             if constexpr (N == 1) {
                 L.row[J] = rA[J];
             } else {
@@ -185,7 +202,7 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uin
                 for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
             }
         }
-        lu_put_row<I, K + 1>(rA, pmw, gb, L);
+        lu_put_row<I, K + 1, CH>(rA, pmw, gb, L);
     }
 }
 
@@ -206,13 +223,13 @@ struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work cou
 
 // a_j -= l * u_j for the groups K.. of step I (the caller is inside the
 // below-the-pivot exec region)
-template <int I, int K>
+template <int I, int K, int CH>
 __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, uint32_t gb,
                                           const LUBuf &L HC_LU_WORK_ARG) {
-    using C = LuChunks<LU_CHUNK>;
+    using C = LuChunks<CH>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (__builtin_expect(group_live<I, K>(pmw, gb), 1)) {
+        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
             HC_LU_WORK(N);
             cf u[N];
             if constexpr (N == 1) {
@@ -228,7 +245,7 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        lu_update<I, K + 1>(rA, l, pmw, gb, L HC_LU_WORK_PASS);
+        lu_update<I, K + 1, CH>(rA, l, pmw, gb, L HC_LU_WORK_PASS);
     }
 }
 
@@ -237,7 +254,7 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
 // finite or that met a pivot outside the fast reciprocal range): every column
 // group and the IEEE reciprocal.  The sparse solve carries no dense tests: it
 // reports such a solve, and the caller solves the system again densely.
-template <int I, bool DENSE>
+template <int I, bool DENSE, int CH>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
                                              bool is_piv, float piv_abs, int pl0, int pl1 HC_LU_WORK_ARG) {
     constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
@@ -248,10 +265,10 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         const uint32_t pp1 = (uint32_t)__builtin_amdgcn_readlane((int)pat, pl1);
         pmw = (pp0 | pp1) & FULL;
     }
-    const uint32_t gb = group_bits(pmw);
+    const uint32_t gb = group_bits<CH>(pmw);
     if (is_piv) {                                          // pivot row -> buffer
         L.row[I] = rA[I];
-        lu_put_row<I, 0>(rA, pmw, gb, L);
+        lu_put_row<I, 0, CH>(rA, pmw, gb, L);
         L.row[30] = rB;
         L.row[31].x = __int_as_float(rowid);
     }
@@ -290,14 +307,14 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         rB = cmk(bp.x, bp.y);
         // v_bfe_i32 + v_and_or_b32
         if constexpr (!DENSE) pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-        lu_update<I, 0>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
+        lu_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
     }
 }
 
 // One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
 // outside the fast reciprocal range sets `redo` (the solve goes on with
 // garbage, the caller discards it and solves densely).
-template <int I, bool DENSE>
+template <int I, bool DENSE, int CH>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
                                            bool row_lane, PivF &my, LUBuf &L, bool &redo HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
@@ -317,14 +334,22 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         if (__builtin_expect(rare, 0)) {
             // rare: NaN at position I wins (:57-64); exact ties: first position wins
             const bool isn = v != v;
-            const int key2 = (elig && !isn) ? __float_as_int(v) : -1;
-            const int mx2 = half_max_int_p16(key2);
-            const unsigned long long m2 = __builtin_amdgcn_ballot_w64(key2 == mx2);
-            const unsigned long long nanm = __builtin_amdgcn_ballot_w64(isn) & __builtin_amdgcn_ballot_w64(rowid == I);
+            const unsigned long long nanb = __builtin_amdgcn_ballot_w64(isn);
+            // the maximum over the non-NaN candidates: the first search's unless
+            // some lane holds a NaN (ties and out-of-range pivots need no second
+            // reduction)
+            int mx2 = mx;
+            unsigned long long m2 = m;
+            if (__builtin_expect(nanb != 0ull, 0)) {
+                const int key2 = (elig && !isn) ? __float_as_int(v) : -1;
+                mx2 = half_max_int_p16(key2);
+                m2 = __builtin_amdgcn_ballot_w64(key2 == mx2);
+            }
+            const unsigned long long nanm = nanb & __builtin_amdgcn_ballot_w64(rowid == I);
             const unsigned nlo = (unsigned)nanm, nhi = (unsigned)(nanm >> 32);
             const unsigned mine_m = hb ? (unsigned)(m2 >> 32) : (unsigned)m2, mine_n = hb ? nhi : nlo;
             const int c2 = ((mine_m >> r) & 1u) ? rowid : (1 << 20);
-            const int mn = half_min_i(c2);
+            const int mn = half_min_int_p16(c2);
             const unsigned long long w = __builtin_amdgcn_ballot_w64(row_lane && rowid == mn);
             const unsigned wm = hb ? (unsigned)(w >> 32) : (unsigned)w;
             const int pl = mine_n ? hb + __builtin_ctz(mine_n) : hb + (wm ? __builtin_ctz(wm) : 0);
@@ -341,8 +366,8 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl0 = __builtin_ctz(mlo);        // exactly one bit per half here
             pl1 = 32 + __builtin_ctz(mhi);
         }
-        lu_step_body<I, DENSE>(rA, rB, rowid, pat, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
-        lu_forward<I + 1, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo HC_LU_WORK_PASS);
+        lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
+        lu_forward<I + 1, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo HC_LU_WORK_PASS);
     }
 }
 
@@ -389,7 +414,7 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 // not provably finite or a pivot outside the fast reciprocal range: the
 // caller then rebuilds the system and calls the DENSE solve, the reference
 // algorithm step for step (both exact).
-template <bool DENSE>
+template <bool DENSE, int CH = LU_CHUNK>
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, bool &redo,
                                       unsigned long long count_mask = ~0ull) {
     (void)count_mask;   // diagnostic builds (HC_DIAG_LUWORK): lanes whose executed work is counted
@@ -419,7 +444,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
     LuWork lu_work_acc{0ull, count_mask};
-    lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo, lu_work_acc);
+    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
     if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
@@ -427,7 +452,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     }
     if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
-    lu_forward<0, DENSE>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
+    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
     pf2 res = {0.0f, 0.0f};
