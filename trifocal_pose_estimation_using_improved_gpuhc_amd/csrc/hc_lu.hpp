@@ -376,8 +376,9 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
 // lanes of its half with v_readlane (owner lane of each half found by a
 // ballot of the final row ids), and lanes I and 32 + I -- which return x_I --
 // capture it with one exec-masked move (static lanes: no compare, no select,
-// no LDS redistribution at the end).  The owner's rB is final at its step:
-// later steps J < I update only rows at positions below J.
+// no LDS redistribution at the end).  The owner's rB is final at its step
+// (every step J > I has updated it) and dead after it, so the later steps
+// J < I may update it unmasked.
 template <int I>
 __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, pf2 &res) {
     if constexpr (I >= 0) {
@@ -399,7 +400,10 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
                      "v_mov_b64 %0, %4\n\ts_mov_b32 exec_lo, %5\n\ts_mov_b32 exec_hi, %5\n\t"
                      "v_mov_b64 %1, %0\n\ts_mov_b64 exec, %2"
                      : "=&v"(xv), "+v"(res), "=&s"(tmp) : "s"(xs0), "s"(xs1), "i"(1u << I));
-        if (rowid < I) {
+        // rows above position I take b -= x_I * a_I; the update runs unmasked
+        // (no compare, no exec region): the rows at or below I are solved, so
+        // their rB is dead (profiles/r3aa_ab_backsub_unmasked.jsonl)
+        if constexpr (I > 0) {
             const pf2 w = pcmsub(pf2{rB.x, rB.y}, xv, pf2{rA[I].x, rA[I].y});
             rB = cmk(w.x, w.y);
         }
