@@ -38,31 +38,49 @@ sys.path.insert(0, ROOT)
 FLOP_PRED_STAGE = 104.3e3    # Hx 12,276 + Ht 12,960 + LU 78,670 + axpys ~360
 FLOP_CORR_STAGE = 101.3e3    # Hx 12,276 + H 10,080 + LU 78,670 + update/norms ~300
 # The LU's rank-1 updates are 8555 element updates (8 FLOP each = 68,440 FLOP)
-# of the 78,670 in the dense algorithm the reference runs.  The structurally
+# of the 78,670 in the dense algorithm the reference runs; the structurally
 # sparse LU executes only the column groups that are non-zero in a pivot row
-# of the wave (0.589 of dense with groups of 4 columns, round 3 first half), measured
-# by the HC_DIAG_LUWORK build (scripts/lu_work.py, profiles/*_lu_work.json; read
-# by lu_executed_fraction, since it depends on the LU's column-group size).
+# of the wave.  `frac_executed_lu` prices the updates as executed, with the
+# executed fraction measured by the HC_DIAG_LUWORK build of the same sources
+# (scripts/lu_work.py, profiles/*_lu_work.json stamped with the product build id).
 LU_UPDATE_DENSE_FLOP = 68440.0
 
 
-def lu_executed_fraction():
-    """Executed fraction of the dense rank-1 update work, from the newest
-    committed config-2 HC_DIAG_LUWORK measurement of the kernel
-    (profiles/*_lu_work.json; the fraction depends on the LU's column-group
-    size): (fraction, file)."""
+def _profiles_of_build(pattern, bid, pick):
+    """(value, file) from the committed profiles matching `pattern` whose
+    build_id is `bid` (the loaded library's _abi.build_id()); (None, reason)
+    when no profile measured this build.  Newest by the recorded timestamp."""
     import glob
-    best = (0.5891, "profiles/r3j_lu_work.json")
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_lu_work.json"))):
-        if "scaled" in os.path.basename(f):
-            continue
+    found = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", pattern)):
         try:
             with open(f) as fh:
-                d = json.loads([ln for ln in fh.read().splitlines() if ln.startswith("{")][-1])
-            best = (float(d["executed_fraction"]), os.path.relpath(f, ROOT))
-        except (OSError, ValueError, KeyError, IndexError):
+                txt = fh.read()
+        except OSError:
             continue
-    return best
+        try:
+            d = json.loads(txt)
+        except ValueError:
+            try:
+                d = json.loads([ln for ln in txt.splitlines() if ln.startswith("{")][-1])
+            except (ValueError, IndexError):
+                continue
+        if d.get("build_id") != bid:
+            continue
+        v = pick(d)
+        if v is not None:
+            found.append((d.get("measured_at", ""), v, os.path.relpath(f, ROOT)))
+    if not found:
+        return None, f"no profiles/{pattern} of build {bid}"
+    found.sort()
+    return found[-1][1], found[-1][2]
+
+
+def lu_executed_fraction(bid):
+    """Executed fraction of the dense rank-1 update work on config 2, from the
+    HC_DIAG_LUWORK profile of this build: (fraction, file) or (None, reason)."""
+    return _profiles_of_build("*_lu_work.json", bid,
+                              lambda d: None if "scaled" in d.get("config", "") else d.get("executed_fraction"))
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak (64 FLOP/clk/SIMD) == FP32 MFMA peak
 HBM_PEAK_GBS = 8000.0
 TRACK_KERNEL = "void hc::k_track<false, 5, true, false>(hc::KArgs)"
@@ -79,6 +97,8 @@ def parse():
                     help="samples in the bounded CPU baseline run (~15 s on 16 host cores)")
     ap.add_argument("--abort-samples", type=int, default=1000,
                     help="samples per GPU of the early-abort (config 3/4) time-to-first-good-pose run; 0 disables")
+    ap.add_argument("--abort-repeats", type=int, default=12,
+                    help="runs per abort semantics in the early-abort leg (median, min and max reported)")
     ap.add_argument("--abort-chunk", type=int, default=125,
                     help="samples per launch in the early-abort run (the cross-GPU flag is reduced between launches)")
     ap.add_argument("--noisy-trials", type=int, default=10,
@@ -241,8 +261,10 @@ def main():
     steps_sum = int(host["stats"]["steps"].astype(np.int64).sum())
     corr_sum = int(host["stats"]["corrections"].astype(np.int64).sum())
     flops = steps_sum * 4 * FLOP_PRED_STAGE + corr_sum * FLOP_CORR_STAGE          # dense-LU convention
-    lu_frac, lu_frac_src = lu_executed_fraction()
-    flops_exec = flops - (steps_sum * 4 + corr_sum) * LU_UPDATE_DENSE_FLOP * (1.0 - lu_frac)   # LU updates as executed
+    bid = _abi.build_id()
+    lu_frac, lu_frac_src = lu_executed_fraction(bid)
+    flops_exec = None if lu_frac is None else \
+        flops - (steps_sum * 4 + corr_sum) * LU_UPDATE_DENSE_FLOP * (1.0 - lu_frac)   # LU updates as executed
     from trifocal_pose_estimation_using_improved_gpuhc_amd import count_solutions
     counts = count_solutions(host["tracks"], host["converge"], host["infinity"])
 
@@ -272,12 +294,13 @@ def main():
         # within a path of any GPU's find, not at its next chunk boundary
         peer = sharding.SharedFlag(device=dev) if world > 1 else None
         if peer is not None:
+            abort_info["cross_rank_flag_memory"] = peer.memory_kind
             abort_info["cross_rank_stop"] = ("device flag over xGMI (hipIpc) + RCCL all_reduce at chunk boundaries"
                                              if peer.ptr is not None else
                                              f"RCCL all_reduce at chunk boundaries only ({peer.error})")
         for inflight in (False, True):
             ttfp, wall, tracked = [], [], []
-            for _ in range(3):
+            for _ in range(args.abort_repeats):
                 tr.reset_tracks(ra)
                 torch.cuda.synchronize(dev)
                 if peer is not None:
@@ -307,10 +330,14 @@ def main():
                 tracked.append(n_tr)
             found = bool(ra.found.item())
             key = "inflight_stop" if inflight else "reference_semantics"
+            ok = [f for f in ttfp if f >= 0]
+            spread = lambda v: {"median": round(float(np.median(v)) * 1e3, 3),  # noqa: E731
+                                "min": round(float(np.min(v)) * 1e3, 3), "max": round(float(np.max(v)) * 1e3, 3)}
             abort_info[key] = {
                 "found": found,
-                "time_to_first_good_pose_ms": round(float(np.median(ttfp)) * 1e3, 3) if found else None,
-                "kernel_exit_wall_ms": round(float(np.median(wall)) * 1e3, 3),
+                "runs": len(ttfp),
+                "time_to_first_good_pose_ms": spread(ok) if ok else None,
+                "kernel_exit_wall_ms": spread(wall),
                 "paths_tracked": int(np.median(tracked))}
         if peer is not None:
             peer.close()
@@ -326,9 +353,9 @@ def main():
 
     if rank == 0:
         med_launch_s = float(np.median(launch_ms)) / 1e3
-        achieved_tf = flops_exec / med_launch_s / 1e12
-        achieved_dense_tf = flops / med_launch_s / 1e12
-        traffic, traffic_src = traffic_bytes(TRACK_KERNEL)
+        achieved_tf = flops / med_launch_s / 1e12                  # the reference's (dense) LU
+        achieved_exec_tf = None if flops_exec is None else flops_exec / med_launch_s / 1e12
+        traffic, traffic_src = traffic_bytes(TRACK_KERNEL, bid)
         line = {
             "metric": "HC paths/sec (312 tracks x RANSAC samples)",
             "value": round(value, 1),
@@ -359,7 +386,8 @@ def main():
                        "parallelism": f"samples sharded over {world} GPU(s), no data-path collective",
                        "GPUHC_Max_Steps": tr.settings.max_steps,
                        "GPUHC_Max_Correction_Steps": tr.settings.max_corrections,
-                       "kernel": _abi.lib().hc_trifocal_version().decode()},
+                       "kernel": _abi.lib().hc_trifocal_version().decode(),
+                       "build_id": bid},
             "roofline": {"bound": "valu_fp32", "achieved": round(achieved_tf, 3), "peak": FP32_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                          "traffic": traffic,
@@ -367,20 +395,24 @@ def main():
                          "traffic_unit": "HBM bytes per launch of the same kernel (rocprofv3 FETCH_SIZE x2 gfx950 "
                                          "correction + WRITE_SIZE, separate --pmc passes, scripts/profile.sh); "
                                          "algorithmic ~0.5 KB/path = 15.3 MB/launch",
-                         "achieved_dense_lu": round(achieved_dense_tf, 3),
-                         "frac_dense_lu": round(achieved_dense_tf / FP32_PEAK_TFLOPS, 4),
                          "note": "FP32 VALU-issue/latency bound tracker kernel (no GEMM: 30x30 complex LUs of "
-                                 "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = FLOPs of "
-                                 "the executed stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 kFLOP / "
-                                 "corrector stage, with the LU's rank-1 updates counted over the column groups "
-                                 "the structurally sparse LU executes: lu_executed_fraction of the dense 68.4 "
-                                 "kFLOP, measured by the HC_DIAG_LUWORK build in lu_executed_fraction_source) / "
+                                 "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = algorithmic "
+                                 "FLOPs of the launch's stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 "
+                                 "kFLOP / corrector stage, the LU priced as the reference's dense algorithm) / "
                                  "median single-launch kernel time (HIP events on the launch stream). "
-                                 "achieved_dense_lu prices the LU as the reference's dense algorithm.",
-                         "lu_executed_fraction": round(lu_frac, 4),
+                                 "achieved_executed_lu prices the LU's rank-1 updates over the column groups the "
+                                 "structurally sparse LU executes (lu_executed_fraction of the dense 68.4 kFLOP, "
+                                 "measured by the HC_DIAG_LUWORK build of this build's sources, "
+                                 "lu_executed_fraction_source): the stricter figure.  traffic and the LU fraction "
+                                 "come only from profiles stamped with this build_id (null with the reason "
+                                 "otherwise).",
+                         "achieved_executed_lu": None if achieved_exec_tf is None else round(achieved_exec_tf, 3),
+                         "frac_executed_lu": None if achieved_exec_tf is None else
+                         round(achieved_exec_tf / FP32_PEAK_TFLOPS, 4),
+                         "lu_executed_fraction": None if lu_frac is None else round(lu_frac, 4),
                          "lu_executed_fraction_source": lu_frac_src,
                          "kernel_ms": round(float(np.median(launch_ms)), 4),
-                         "executed_gflop_per_launch": round(flops_exec / 1e9, 3),
+                         "executed_gflop_per_launch": None if flops_exec is None else round(flops_exec / 1e9, 3),
                          "dense_lu_gflop_per_launch": round(flops / 1e9, 3),
                          "rk4_steps": steps_sum, "corrections": corr_sum},
             "solutions": {"converged": counts[0], "real": counts[1], "infinity": counts[2]},
@@ -476,20 +508,13 @@ def noisy_pose_leg(args, tr, problem, data, world, rank, dev, stream):
             "median_candidates": int(np.median(cands))}
 
 
-def traffic_bytes(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (PMC counters cannot be collected inside the timed run): (bytes, file)."""
-    import glob
-    best, src = None, None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_summary.json"))):
-        try:
-            with open(f) as fh:
-                d = json.load(fh)
-        except (OSError, ValueError):
-            continue
-        if d.get("kernel") == kernel and "hbm_bytes_per_launch" in d.get("derived", {}):
-            best, src = d["derived"]["hbm_bytes_per_launch"], os.path.relpath(f, ROOT)
-    return best, src
+def traffic_bytes(kernel, bid):
+    """HBM bytes per launch of `kernel` from the PMC summary of this build
+    (PMC counters cannot be collected inside the timed run): (bytes, file) or
+    (None, reason)."""
+    return _profiles_of_build("*_pmc_summary.json", bid,
+                              lambda d: d.get("derived", {}).get("hbm_bytes_per_launch")
+                              if d.get("kernel") == kernel else None)
 
 
 def cpu_info():

@@ -125,9 +125,9 @@ typedef struct {
 size_t hc_trifocal_workspace_size(void);
 
 /* Workspace size that also enables time slicing for launches of up to
-   sub_ransac_iters samples at GPUHC_Max_Steps = 80: 1 KB + (256 + 8 x 28)
+   sub_ransac_iters samples at GPUHC_Max_Steps = 80: 33 KB + (256 + 8 x 28)
    bytes per path more (a suspended path's 256-byte state block and the resume
-   ring, one entry per suspension).  With it, a path that has run a
+   ring, one entry per suspension plus 4096 spare entries).  With it, a path that has run a
    slice of steps while other paths wait is suspended at a step boundary and
    resumed after the new paths (same results bit for bit; every path starts
    early, so a launch no longer ends with long paths that were dequeued late).
@@ -157,14 +157,21 @@ hcStatus hc_trifocal_2op1p_30x30_track_abort(const hcTrackArgs *args, const hcAb
                                              hcStream stream);
 
 /* The cross-process early-stop flag of hcAbortArgs::peer_found.  It lives in
-   the creating process's device memory (hipMalloc + hipIpcGetMemHandle); the
-   64-byte handle travels to the other processes (e.g. a torch.distributed
-   broadcast), which map it with hc_shared_flag_open (hipIpcOpenMemHandle, peer
-   access over xGMI).  create zeroes it; reset zeroes it on a stream before a
-   new run (the caller orders the reset before any rank's launch);
-   close(flag, opened = 1 for a handle opened here, 0 for the creator's). */
+   the creating process's device memory, allocated uncached
+   (hipExtMallocWithFlags(hipDeviceMallocUncached): coherent across devices
+   while kernels run; fine-grained, then plain hipMalloc, if the device cannot
+   export those with hipIpcGetMemHandle); the 64-byte handle travels to the
+   other processes (e.g. a torch.distributed broadcast), which map it with
+   hc_shared_flag_open (hipIpcOpenMemHandle, peer access over xGMI).  create
+   zeroes it; reset zeroes it on a stream before a new run (the caller orders
+   the reset before any rank's launch); close(flag, opened = 1 for a handle
+   opened here, 0 for the creator's).  hc_shared_flag_memory_kind(flag) of a
+   flag created in this process: 2 uncached, 1 fine-grained, 0 plain
+   (coarse-grained: another device's find may then be seen only at the next
+   synchronisation), -1 not created here. */
 typedef struct { unsigned char reserved[64]; } hcIpcHandle;   /* == hipIpcMemHandle_t */
 hcStatus hc_shared_flag_create(uint32_t **flag, hcIpcHandle *handle);
+int hc_shared_flag_memory_kind(const uint32_t *flag);
 hcStatus hc_shared_flag_open(const hcIpcHandle *handle, uint32_t **flag);
 hcStatus hc_shared_flag_reset(uint32_t *flag, hcStream stream);
 hcStatus hc_shared_flag_close(uint32_t *flag, int opened);
@@ -201,11 +208,15 @@ hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspa
                         whose partner row (lane ^ 16) has more than 10
                         (Evaluations);
      HC_ERROR_DEVICE -- time slicing only: a suspended path could not be handed
-                        over (its ring entry never arrived within the bounded
-                        wait, or the ring overflowed); that path's converge /
+                        over (the ring overflowed: more than 4096 re-pushes of
+                        abandoned tickets in one launch; or a ring entry
+                        outside the launch's paths); that path's converge /
                         infinity / stats / track entry are not final.  The
-                        control block's ring_fail words hold the ticket, the tag
-                        seen, tail and head for diagnosis.
+                        control block's ring_fail words hold the ticket, the
+                        entry seen, tail and head for diagnosis.  (A consumer
+                        that waits too long for a ring entry abandons the
+                        ticket and its pusher pushes the path again: a paused
+                        wave delays a path, it never loses it.)
    Blocking read -- call after synchronising. */
 hcStatus hc_trifocal_workspace_status(const void *workspace);
 
@@ -246,6 +257,20 @@ const char *hc_last_error_string(void);
 
 /* Library / kernel identification (for logs and the bench JSON). */
 const char *hc_trifocal_version(void);
+
+/* Layout version of the structs of this header.  A caller compares
+   hc_trifocal_abi_version() with the HC_TRIFOCAL_ABI_VERSION it was built
+   against before its first launch (the Python binding and the reference-named
+   shim do): a library of another version reads the argument structs
+   differently (version 2 appended hcAbortArgs::peer_found). */
+#define HC_TRIFOCAL_ABI_VERSION 2
+int hc_trifocal_abi_version(void);
+
+/* Tests only: every 16th ring ticket of later sliced launches in this process
+   waits delay_ticks (device clock ticks, 100 MHz) between its ticket and its
+   entry, and consumers abandon a ticket after delay_ticks / 8 instead of 1 ms,
+   so that the abandon / re-push hand-over runs; 0 restores the default. */
+void hc_trifocal_set_ring_test(int delay_ticks);
 
 #ifdef __cplusplus
 }

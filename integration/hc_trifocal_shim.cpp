@@ -68,9 +68,22 @@ bool ensure(StreamState &st, hipStream_t s, size_t need, bool need_unified) {
     return st.workspace && (!need_unified || st.unified);
 }
 
+// the library must read the argument structs as this shim lays them out
+bool abi_ok() {
+    static const bool ok = [] {
+        const int v = hc_trifocal_abi_version();
+        if (v != HC_TRIFOCAL_ABI_VERSION)
+            printf("hc_trifocal_shim: library ABI %d, shim built against %d: not launching\n", v,
+                   HC_TRIFOCAL_ABI_VERSION);
+        return v == HC_TRIFOCAL_ABI_VERSION;
+    }();
+    return ok;
+}
+
 // the stream's state for a launch of N samples (N = 0: abort mode, the base
 // size); reserved streams return at once
 StreamState *state_for(hipStream_t s, bool need_unified, int N = 0, int max_steps = 80) {
+    if (!abi_ok()) return nullptr;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     std::lock_guard<std::mutex> g(g_mu);
@@ -159,7 +172,7 @@ real_Double_t track_abort(magma_queue_t q, int N, int E, int max_steps, int max_
 }  // namespace
 
 extern "C" hcStatus hc_trifocal_shim_reserve(magma_queue_t queue, int max_samples, int max_steps) {
-    if (!queue || max_samples < 0 || max_steps < 0) return HC_ERROR_INVALID_VALUE;
+    if (!queue || max_samples < 0 || max_steps < 0 || !abi_ok()) return HC_ERROR_INVALID_VALUE;
     const hipStream_t s = magma_queue_get_hip_stream(queue);
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return HC_ERROR_DEVICE;

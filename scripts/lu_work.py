@@ -17,6 +17,7 @@ import ctypes as C
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -61,7 +62,11 @@ def main():
            "executed_update_elements": elems,
            "executed_update_elements_per_solve": elems / max(1, solves),
            "dense_update_elements_per_solve": DENSE_UPDATE_ELEMENTS,
-           "executed_fraction": elems / max(1, solves) / DENSE_UPDATE_ELEMENTS}
+           "executed_fraction": elems / max(1, solves) / DENSE_UPDATE_ELEMENTS,
+           # the product build of the same sources (bench.py prices its LU with this file)
+           "build_id": _abi.build_id(_abi.PRODUCT_LIB_PATH),
+           "diag_build_id": _abi.build_id(),
+           "measured_at": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}
     print(json.dumps(res))
 
 

@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile.sh run: per-launch PMC counters of the tracker
-kernel plus derived utilisations.  usage: pmc_summary.py TAG [out.json] [kernel version string]"""
+kernel plus derived utilisations, stamped with the build id of the library the
+run loaded (the bench line's config.build_id in the trace log), which is how
+bench.py finds the profile of its own build.  usage: pmc_summary.py TAG [out.json]"""
 import collections
 import csv
 import glob
@@ -16,7 +18,7 @@ base = os.path.join(ROOT, "gpurun_out")
 KNAME = os.environ.get("HC_PMC_KERNEL", "void hc::k_track<false, 5, true, false>(hc::KArgs)")
 stats = list(csv.DictReader(open(os.path.join(base, f"{tag}_trace", "run_kernel_stats.csv"))))
 trk = [r for r in stats if r["Name"] == KNAME][0]
-out = {"tag": tag, "version": sys.argv[3] if len(sys.argv) > 3 else None, "kernel": trk["Name"], "calls": int(trk["Calls"]), "avg_ns": float(trk["AverageNs"]),
+out = {"tag": tag, "build_id": None, "measured_at": None, "kernel": trk["Name"], "calls": int(trk["Calls"]), "avg_ns": float(trk["AverageNs"]),
        "min_ns": float(trk["MinNs"]), "max_ns": float(trk["MaxNs"]), "counters": {}}
 meta = None
 for d in sorted(glob.glob(os.path.join(base, f"{tag}_pmc*"))):
@@ -65,8 +67,15 @@ if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
     der["hbm_bytes_per_launch"] = der["hbm_fetch_bytes_corrected"] + der["hbm_write_bytes"]
 # FLOPs of the same bench run (its JSON line in the trace log): FLOP per VALU instruction
 try:
+    import time
     lines = [l for l in open(os.path.join(base, f"{tag}_trace.log")) if l.startswith("{")]
-    rl = json.loads(lines[-1])["roofline"]
+    bl = json.loads(lines[-1])
+    out["build_id"] = bl["config"].get("build_id")
+    out["measured_at"] = time.strftime("%Y-%m-%dT%H:%M:%SZ",
+                                       time.gmtime(os.path.getmtime(os.path.join(base, f"{tag}_trace.log"))))
+    out["bench_ms_per_step"] = bl.get("ms_per_step")
+    out["bench_kernel_ms"] = bl["roofline"].get("kernel_ms")
+    rl = bl["roofline"]
     if "SQ_INSTS_VALU" in c:
         ex = rl.get("executed_gflop_per_launch")
         de = rl.get("dense_lu_gflop_per_launch", rl.get("algorithmic_gflop_per_launch"))

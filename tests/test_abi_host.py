@@ -67,12 +67,25 @@ def test_workspace_size_and_version():
     assert b"gfx950" in L.hc_trifocal_version()
 
 
+def test_abi_version_and_build_id():
+    """The binding refuses a library of another struct layout; the build id
+    names the library's device code (bench.py selects its profiles by it)."""
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+    L = _abi.lib()
+    assert L.hc_trifocal_abi_version() == _abi.ABI_VERSION == 2
+    hdr = open(os.path.join(ROOT, "include", "hc_trifocal.h")).read()
+    assert "#define HC_TRIFOCAL_ABI_VERSION 2" in hdr
+    bid = _abi.build_id()
+    assert bid.startswith("v") and "+" in bid and len(bid.split("+")[1]) == 12
+    assert bid == _abi.build_id(_abi.PRODUCT_LIB_PATH)
+
+
 def test_workspace_size_for_time_slicing():
     """hc_trifocal_workspace_size_for(N): the base workspace + the time-slicing
     area: ring counters (1 KB), a 256-B suspend block per path and an 8-B ring
     entry per possible suspension -- at most (max_steps + 1) / 3 per path,
-    never reused within a launch (+1 per path, +64).  The plain form assumes
-    max_steps = 80."""
+    never reused within a launch (+1 per path, + 4096 spare entries for the
+    re-pushes of abandoned tickets).  The plain form assumes max_steps = 80."""
     from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
     L = _abi.lib()
     base = int(L.hc_trifocal_workspace_size())
@@ -80,7 +93,7 @@ def test_workspace_size_for_time_slicing():
     assert base < s0 <= s1 < s100
     assert s100 % 256 == 0
     per_path = 256 + 8 * (81 // 3 + 1)
-    assert per_path * 312 * 100 <= s100 - base <= per_path * 312 * 100 + 4096
+    assert per_path * 312 * 100 + 8 * 4096 <= s100 - base <= per_path * 312 * 100 + 8 * 4096 + 2048
     assert int(L.hc_trifocal_workspace_size_for(-5)) == s0
     assert int(L.hc_trifocal_workspace_size_for_steps(100, 80)) == s100
     s200 = int(L.hc_trifocal_workspace_size_for_steps(100, 200))

@@ -153,9 +153,10 @@ def _rank_main_shared_flag(rank, world, port, out_dir):
         h = r.host()
         dist.barrier()
         flag.close()
+        kind = flag.memory_kind
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), off=off, cnt=cnt, nchunks=len(parts),
                  tracks=h["tracks"], conv=h["converge"], steps=h["stats"]["steps"],
-                 batch_index=h["batch_index"], found=h["found"])
+                 batch_index=h["batch_index"], found=h["found"], kind=str(kind))
     finally:
         dist.destroy_process_group()
 
@@ -188,6 +189,10 @@ def test_two_ranks_shared_flag_stops_other_rank_mid_launch(tmp_path, oracle, ran
         ids = np.nonzero(x["batch_index"] >= 0)[0]
         assert set(int(b) + base for b in ids) <= passing
     r0, r1 = R
+    # the owner's flag is in memory that is coherent across devices while
+    # kernels run (uncached; fine-grained where the device cannot export that)
+    assert str(r0["kind"]) in ("uncached", "fine-grained"), str(r0["kind"])
+    assert str(r1["kind"]) == "None"
     assert len(np.nonzero(r1["batch_index"] >= 0)[0]) > 0 and bool(r1["found"])
     assert len(np.nonzero(r0["batch_index"] >= 0)[0]) == 0
     assert bool(r0["found"])          # the chunk-boundary reduction still delivers the byte

@@ -14,6 +14,9 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # scripts/build_variant.sh)
 LIB_PATH = os.environ.get("HC_TRIFOCAL_LIB") or os.path.join(PKG_DIR, "lib", "libhc_trifocal.so")
 
+# include/hc_trifocal.h HC_TRIFOCAL_ABI_VERSION: the struct layouts below
+ABI_VERSION = 2
+
 NUM_VARS, NUM_PARAMS, NUM_TRACKS = 30, 33, 312
 NPP = NUM_PARAMS + 1
 UNIFIED_INDEX_SIZE = 38880
@@ -86,6 +89,11 @@ def lib() -> C.CDLL:
         # instead of pulling a second HIP/HSA runtime from /opt/rocm.
         import torch  # noqa: F401
         L = C.CDLL(LIB_PATH)
+        L.hc_trifocal_abi_version.restype = C.c_int
+        if L.hc_trifocal_abi_version() != ABI_VERSION:
+            raise HCError(f"{LIB_PATH}: ABI {L.hc_trifocal_abi_version()}, this binding expects {ABI_VERSION}")
+        L.hc_trifocal_set_ring_test.restype = None
+        L.hc_trifocal_set_ring_test.argtypes = [C.c_int]
         L.hc_trifocal_workspace_size.restype = C.c_size_t
         L.hc_trifocal_workspace_size_for.restype = C.c_size_t
         L.hc_trifocal_workspace_size_for.argtypes = [C.c_int]
@@ -139,6 +147,8 @@ def lib() -> C.CDLL:
             L.hc_shared_flag_open.argtypes = [C.POINTER(hcIpcHandle), C.POINTER(C.c_void_p)]
             L.hc_shared_flag_reset.argtypes = [C.c_void_p, C.c_void_p]
             L.hc_shared_flag_close.argtypes = [C.c_void_p, C.c_int]
+            L.hc_shared_flag_memory_kind.restype = C.c_int
+            L.hc_shared_flag_memory_kind.argtypes = [C.c_void_p]
         _lib = L
     return _lib
 
@@ -154,11 +164,52 @@ DECLARED_SYMBOLS = (
     "hc_trifocal_workspace_size", "hc_trifocal_workspace_size_for", "hc_trifocal_workspace_size_for_steps", "hc_trifocal_2op1p_30x30_track", "hc_trifocal_2op1p_30x30_track_abort",
     "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
     "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
-    "hc_last_error_string",
+    "hc_last_error_string", "hc_trifocal_abi_version", "hc_trifocal_set_ring_test",
     "hc_shared_flag_create", "hc_shared_flag_open", "hc_shared_flag_reset", "hc_shared_flag_close",
+    "hc_shared_flag_memory_kind",
     "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",
     "hc_count_triplet_edgels", "hc_read_triplet_edgels", "hc_split_samples", "hc_prepare_target_params",
     "hc_count_solutions",
     "hc_trifocal_pose_support", "hc_pose_merge", "hc_pose_residuals", "hc_write_converged_sols",
     "hc_add_pixel_noise", "hc_write_triplet_edgels",
 )
+
+
+def _fatbin_digest(path: str) -> str | None:
+    """sha256 of the .hip_fatbin section of an ELF shared library: the gfx950
+    code objects of every kernel, independent of the host code around them."""
+    import hashlib
+    import struct
+    with open(path, "rb") as fh:
+        elf = fh.read()
+    if elf[:4] != b"\x7fELF" or elf[4] != 2:
+        return None
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+    def sec(i):
+        name, _typ, _flags, _addr, off, size = struct.unpack_from("<IIQQQQ", elf, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = elf.index(b"\0", stroff + name)
+        if elf[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(elf[off:off + size]).hexdigest()
+    return None
+
+
+def build_id(path: str | None = None) -> str:
+    """Identifies the kernels a profile or bench line measured: the library's
+    version tag and the first 12 hex digits of the sha256 of its device code
+    (.hip_fatbin).  Profiles under profiles/ carry it and bench.py takes its
+    PMC / LU-work sources only from profiles of the loaded build."""
+    import re
+    path = path or LIB_PATH
+    with open(path, "rb") as fh:
+        m = re.search(rb"hc_trifocal gfx950 (v[0-9.]+)", fh.read())
+    ver = m.group(1).decode() if m else "v?"
+    d = _fatbin_digest(path)
+    return f"{ver}+{d[:12] if d else 'nofatbin'}"
+
+
+PRODUCT_LIB_PATH = os.path.join(PKG_DIR, "lib", "libhc_trifocal.so")

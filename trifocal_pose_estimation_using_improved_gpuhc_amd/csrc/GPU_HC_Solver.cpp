@@ -260,7 +260,9 @@ void GPU_HC_Solver::Set_RANSAC_Abort_Arrays() {
     // Abort_Across_GPUs (not in the reference, which keeps one flag per GPU,
     // GPU_HC_Solver.cpp:308-333): a 4-byte flag on the first GPU's device that
     // every GPU's launch sets on a find and polls before each path
-    // (hcAbortArgs::peer_found, system-scope atomics over xGMI)
+    // (hcAbortArgs::peer_found, system-scope atomics over xGMI).  Uncached
+    // device memory: coherent across devices while the kernels run (plain
+    // hipMalloc memory is coherent only at synchronisation points)
     if (Abort_Across_GPUs && !gpus_.empty() && !d_peer_found) {
         const int dev0 = gpus_[0]->dev;
         for (PerGPU *p : gpus_) {
@@ -271,7 +273,10 @@ void GPU_HC_Solver::Set_RANSAC_Abort_Arrays() {
             (void)hipGetLastError();
         }
         HC_HIP_CHECK(hipSetDevice(dev0));
-        HC_HIP_CHECK(hipMalloc(&d_peer_found, 256));
+        if (hipExtMallocWithFlags((void **)&d_peer_found, 256, hipDeviceMallocUncached) != hipSuccess) {
+            (void)hipGetLastError();
+            HC_HIP_CHECK(hipExtMallocWithFlags((void **)&d_peer_found, 256, hipDeviceMallocFinegrained));
+        }
         HC_HIP_CHECK(hipMemset(d_peer_found, 0, 256));
     }
 }

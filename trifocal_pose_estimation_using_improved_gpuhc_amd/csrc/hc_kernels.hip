@@ -59,7 +59,8 @@ struct Workspace {
     unsigned long long t_start;   // s_memrealtime when the first workgroup started (abort mode)
     unsigned long long t_found;   // s_memrealtime of the first good hypothesis
     unsigned ring_fail[4];   // time slicing: ticket, tag seen, tail, head of a ring entry that never came (diagnostics)
-    unsigned pad1[4];
+    unsigned abandoned;      // time slicing: ring tickets abandoned by their consumers (re-pushed; diagnostics)
+    unsigned pad1[3];
     // written by k_prep_tables
     EvalTables tab;
 };
@@ -110,12 +111,27 @@ __host__ __device__ constexpr bool slice_fits(int max_steps, int max_corr, int i
 // its entry while the rest of its kernel runs on -- seen when another stream's
 // first launch created its hardware queue -- and a slot reused meanwhile would
 // lose the suspended path; profiles/r2zb_stress*.jsonl.)
+// RING_SLACK more entries absorb the re-pushes of abandoned tickets (below).
+constexpr unsigned long long RING_SLACK = 4096ull;
 __host__ __device__ constexpr unsigned long long ring_entries(long long paths, int max_steps) {
-    return (unsigned long long)paths * (unsigned long long)((max_steps + 1) / (SLICE_Q > 0 ? SLICE_Q : 1) + 1) + 64ull;
+    return (unsigned long long)paths * (unsigned long long)((max_steps + 1) / (SLICE_Q > 0 ? SLICE_Q : 1) + 1) +
+           RING_SLACK;
 }
-// the longest a consumer waits for a claimed entry whose pusher holds its
-// ticket but has not written it yet (s_memrealtime ticks, 100 MHz: 10 s)
-constexpr unsigned long long RING_WAIT_TICKS = 1000000000ull;
+// How long a consumer waits for a claimed entry whose pusher holds the ticket
+// but has not written it yet before it abandons the ticket (s_memrealtime
+// ticks, 100 MHz: 1 ms).  Abandoning loses nothing: the pusher sees the mark
+// when it writes and pushes the path again on a new ticket (ring_push).
+constexpr unsigned long long RING_ABANDON_TICKS = 100000ull;
+// Every sliced launch's ring entry is written once by one atomic exchange,
+// either by its pusher (the tagged path id) or by a consumer that gave up
+// waiting (the abandon mark: the tag with bit 0 cleared, never a published tag)
+__device__ __forceinline__ unsigned long long ring_abandon_mark(unsigned tag) {
+    return ((unsigned long long)(tag & ~1u) << 32) | 0xFFFFFFFFull;
+}
+// (tests, KArgs::ring_test: consumers abandon after an eighth of the pushers' delay)
+__device__ __forceinline__ unsigned long long ring_wait_ticks(int ring_test) {
+    return ring_test > 0 ? (unsigned long long)(ring_test / 8) : RING_ABANDON_TICKS;
+}
 
 struct KArgs {
     int num_paths;
@@ -144,6 +160,7 @@ struct KArgs {
     int32_t *batch_index;
     // time slicing (slice_q > 0; tracking without abort only)
     int slice_q;
+    int ring_test;                  // tests only (hc_trifocal_set_ring_test): pusher delay in ticks, else 0
     unsigned ring_cap;
     unsigned *rq;                   // ring counters, one 256-B line each: [0] head, [64] tail, [128] avail, [192] meta
     unsigned long long *susp;       // suspend blocks, SUSP_WORDS per path id
@@ -152,8 +169,9 @@ struct KArgs {
 // rq layout: counters zeroed by k_prep_tables every launch; meta: the launch
 // epoch, a magic word and the ring entries already cleared (persist)
 constexpr int RQ_HEAD = 0, RQ_TAIL = 64, RQ_AVAIL = 128, RQ_EPOCH = 192, RQ_MAGIC = 193, RQ_CLEARED = 194,
+              RQ_DLO = 195, RQ_DHI = 196,
               RQ_WORDS = 256;
-constexpr unsigned RQ_MAGIC_VALUE = 0x48435452u;   // "HCTR"
+constexpr unsigned RQ_MAGIC_VALUE = 0x48435432u;   // "HCT2" (the ring-first layout of round 4)
 // tag of ticket t's entry in launch `epoch` (never 0, so a cleared entry never
 // matches; distinct epochs give distinct tags for the same ticket)
 __device__ __forceinline__ unsigned ring_tag(unsigned epoch, unsigned t) {
@@ -198,60 +216,100 @@ __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0
 
 // (pointers and sizes by value: a KArgs reference would put the kernel
 // arguments in scratch memory)
-__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch, int b,
-                                          bool unpaired, Workspace *ws) {
-    const unsigned t = atomicAdd(&rq[RQ_TAIL], 1u);
-    if (t >= cap) {   // cannot happen within the bound of ring_entries (the path would be lost: reported)
-        atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
-        return;
-    }
-    st_u64_h(&ring[t], ((unsigned long long)ring_tag(epoch, t) << 32) | (unsigned)b);
-    if (unpaired) {
-        drain_stores();
-        atomicAdd(&rq[RQ_AVAIL], 1u);
-    }
+__device__ __forceinline__ unsigned long long xchg_u64(unsigned long long *p, unsigned long long v) {
+    return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// the entry of claimed ticket h: its pusher took ticket h before (head never
-// passes tail), so it is written or about to be; a pusher paused mid-push is
-// waited for (bounded: HC_ERROR_DEVICE in the status if it never comes)
-__device__ __forceinline__ int ring_take(const unsigned long long *ring, unsigned cap, unsigned epoch, Workspace *ws,
-                                         unsigned h, const unsigned *rq) {
+// Publishes suspended path b (its block already written and drained).  A
+// pusher that finds its ticket abandoned -- it was paused between taking the
+// ticket and writing the entry for longer than the consumer waits -- pushes
+// again on a new ticket, as an unpaired entry: the consumer of the abandoned
+// ticket looks for a path with an unpaired pop (ring_pop), so this entry must
+// be claimable.  test_delay (tests only): every 16th ticket waits that many
+// ticks before its exchange, so that its consumer abandons it.
+__device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch, int b,
+                                          bool unpaired, Workspace *ws, int test_delay) {
+    for (;;) {
+        const unsigned t = atomicAdd(&rq[RQ_TAIL], 1u);
+        if (t >= cap) {   // more re-pushes than RING_SLACK (the path is lost: reported)
+            atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
+            return;
+        }
+        if (__builtin_expect(test_delay > 0, 0) && (t & 15u) == 7u) {
+            const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - w0 < (unsigned long long)test_delay) __builtin_amdgcn_s_sleep(8);
+        }
+        const unsigned tag = ring_tag(epoch, t);
+        const unsigned long long old = xchg_u64(&ring[t], ((unsigned long long)tag << 32) | (unsigned)b);
+        if (__builtin_expect(old != ring_abandon_mark(tag), 1)) break;
+        unpaired = true;
+    }
+    if (unpaired) atomicAdd(&rq[RQ_AVAIL], 1u);
+}
+// The entry of ticket h: its pusher took ticket h before (head never passes
+// tail), so it is written or about to be.  A pusher paused mid-push is waited
+// for up to wait_ticks; then the ticket is abandoned (-2): one exchange writes
+// the abandon mark, and if the pusher's entry arrived just before it, the
+// exchange returns it and the path is taken after all.  Otherwise the pusher
+// will see the mark and push again (ring_push), so no path is lost.  A path
+// id outside the launch cannot come from the protocol: reported, -1.
+__device__ __forceinline__ int ring_take(unsigned long long *ring, unsigned cap, unsigned epoch, Workspace *ws,
+                                         unsigned h, const unsigned *rq, int num_paths, unsigned long long wait_ticks) {
     if (h >= cap) {
         atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE);
         return -1;
     }
     const unsigned tag = ring_tag(epoch, h);
     unsigned long long e = ld_u64_h(&ring[h]);
-    if ((unsigned)(e >> 32) == tag) return (int)(unsigned)e;
-    const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
-    for (;;) {
-        __builtin_amdgcn_s_sleep(8);
-        e = ld_u64_h(&ring[h]);
-        if ((unsigned)(e >> 32) == tag) return (int)(unsigned)e;
-        if (__builtin_amdgcn_s_memrealtime() - w0 > RING_WAIT_TICKS) break;
+    if ((unsigned)(e >> 32) != tag) {
+        const unsigned long long w0 = __builtin_amdgcn_s_memrealtime();
+        for (;;) {
+            __builtin_amdgcn_s_sleep(8);
+            e = ld_u64_h(&ring[h]);
+            if ((unsigned)(e >> 32) == tag) break;
+            if (__builtin_amdgcn_s_memrealtime() - w0 > wait_ticks) {
+                e = xchg_u64(&ring[h], ring_abandon_mark(tag));
+                if ((unsigned)(e >> 32) == tag) break;
+                atomicAdd(&ws->abandoned, 1u);
+                return -2;
+            }
+        }
     }
+    if ((unsigned)e < (unsigned)num_paths) return (int)(unsigned)e;
     if (atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE) == 0u) {
-        // diagnostics: ticket, tag seen, tail, head
+        // diagnostics: ticket, entry seen, tail, head
         ws->ring_fail[0] = h;
-        ws->ring_fail[1] = (unsigned)(e >> 32);
+        ws->ring_fail[1] = (unsigned)e;
         ws->ring_fail[2] = ld_rlx(&rq[RQ_TAIL]);
         ws->ring_fail[3] = ld_rlx(&rq[RQ_HEAD]);
     }
     return -1;
 }
-__device__ __forceinline__ int ring_pop_paired(unsigned *rq, const unsigned long long *ring, unsigned cap,
-                                               unsigned epoch, Workspace *ws) {
-    return ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
-}
 // oldest suspended path id, or -1 if there is none
-__device__ __forceinline__ int ring_pop(unsigned *rq, const unsigned long long *ring, unsigned cap, unsigned epoch,
-                                        Workspace *ws) {
+__device__ __forceinline__ int ring_pop(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch,
+                                        Workspace *ws, int num_paths, unsigned long long wait_ticks) {
     int *avail = reinterpret_cast<int *>(&rq[RQ_AVAIL]);
-    if (ld_i_rlx(avail) <= 0) return -1;
-    for (;;) {
-        if (atomicSub(avail, 1) > 0) return ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq);
+    // after 16 abandoned tickets this pop gives up (-1: the half
+    // idles); nothing is lost, the abandoned paths' pushers push them again
+    // and keep popping while entries remain
+    for (int tries = 0; tries < 16;) {
+        if (ld_i_rlx(avail) <= 0) return -1;
+        if (atomicSub(avail, 1) > 0) {
+            const int b = ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq, num_paths, wait_ticks);
+            if (b != -2) return b;
+            atomicAdd(avail, 1);   // abandoned: the claim goes back (its entry is still to be popped)
+            tries++;
+            continue;
+        }
         if (atomicAdd(avail, 1) + 1 <= 0) return -1;
     }
+    return -1;
+}
+// the swap's pop, right after its own push (no claim); an abandoned ticket
+// falls back to an unpaired pop
+__device__ __forceinline__ int ring_pop_paired(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch,
+                                               Workspace *ws, int num_paths, unsigned long long wait_ticks) {
+    const int b = ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq, num_paths, wait_ticks);
+    return b != -2 ? b : ring_pop(rq, ring, cap, epoch, ws, num_paths, wait_ticks);
 }
 
 // ---------------------------------------------------------------- table prep
@@ -282,6 +340,7 @@ struct PrepArgs {
     unsigned *rq;                // time slicing, else null
     unsigned long long *ring;
     unsigned ring_cap;
+    unsigned susp_entry0, susp_entry1;   // the suspend blocks' span in ring-entry units (from the ring's start)
 };
 constexpr int PREP_THREADS = 256;
 __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
@@ -291,7 +350,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
     __shared__ int s_len[32];
     __shared__ int s_bad;
     __shared__ unsigned long long s_h[PREP_THREADS];
-    __shared__ unsigned s_cleared;
+    __shared__ unsigned s_cleared, s_dlo, s_dhi;
     __shared__ int s_valid;
     const int tid = threadIdx.x;
     {
@@ -311,7 +370,10 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                               __hip_atomic_load(pa.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
             ws->found = (pa.found_in[0] || peer) ? 1u : 0u;
         }
-        s_cleared = (pa.rq && pa.rq[RQ_MAGIC] == RQ_MAGIC_VALUE) ? pa.rq[RQ_CLEARED] : 0u;
+        const bool known = pa.rq && pa.rq[RQ_MAGIC] == RQ_MAGIC_VALUE;
+        s_cleared = known ? pa.rq[RQ_CLEARED] : 0u;
+        s_dlo = known ? pa.rq[RQ_DLO] : 0u;
+        s_dhi = known ? pa.rq[RQ_DHI] : 0u;
     }
     __syncthreads();
     for (int w = PREP_THREADS / 2; w > 0; w >>= 1) {
@@ -319,8 +381,13 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         __syncthreads();
     }
     const unsigned long long src_hash = s_h[0];
-    if (pa.rq)
+    if (pa.rq) {
+        // entries never cleared, and cleared entries an earlier launch's
+        // suspend blocks overwrote (the dirty range), inside this launch's ring
         for (unsigned e = s_cleared + tid; e < pa.ring_cap; e += PREP_THREADS) pa.ring[e] = 0ull;
+        const unsigned dhi = min(s_dhi, min(s_cleared, pa.ring_cap));
+        for (unsigned e = s_dlo + tid; e < dhi; e += PREP_THREADS) pa.ring[e] = 0ull;
+    }
     if (tid == 0) s_valid = (T->magic == TAB_MAGIC && T->src_hash == src_hash && T->status == 0) ? 1 : 0;
     __syncthreads();
     if (pa.rq && tid == 0) {
@@ -330,7 +397,22 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         rq[RQ_AVAIL] = 0u;
         const unsigned e = (rq[RQ_MAGIC] == RQ_MAGIC_VALUE) ? rq[RQ_EPOCH] + 1u : 1u;
         rq[RQ_EPOCH] = e ? e : 1u;
-        rq[RQ_CLEARED] = s_cleared > pa.ring_cap ? s_cleared : pa.ring_cap;
+        // this launch's suspend blocks start right after its ring: the cleared
+        // entries they may overwrite join the dirty range (one interval that
+        // covers every such range not re-zeroed yet)
+        const unsigned cleared = max(s_cleared, pa.ring_cap);
+        unsigned lo = max(s_dlo, pa.ring_cap), hi = s_dhi;                 // what this launch did not re-zero
+        const unsigned s0 = pa.susp_entry0, s1 = min(cleared, pa.susp_entry1);   // this launch's blocks
+        if (s0 < s1) {
+            const bool had = lo < hi;
+            lo = had ? min(lo, s0) : s0;
+            hi = had ? max(hi, s1) : s1;
+        }
+        if (hi > cleared) hi = cleared;
+        if (lo >= hi) lo = hi = 0u;
+        rq[RQ_CLEARED] = cleared;
+        rq[RQ_DLO] = lo;
+        rq[RQ_DHI] = hi;
         rq[RQ_MAGIC] = RQ_MAGIC_VALUE;
     }
     if (s_valid) return;   // tables built from this index table already
@@ -684,11 +766,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         nb = deq_hint;                       // claimed by the suspension
                     } else if (!ABORT && deq_hint == -2) {
                         nb = a.num_paths;                    // swap: the oldest suspended path
-                        rb = ring_pop_paired(a.rq, a.ring, a.ring_cap, epoch, ws);
+                        rb = ring_pop_paired(a.rq, a.ring, a.ring_cap, epoch, ws, a.num_paths, ring_wait_ticks(a.ring_test));
                     } else {
                         nb = (ABORT || a.slice_q == 0 || ld_rlx(&ws->queue) < (unsigned)a.num_paths)
                                  ? (int)atomicAdd(&ws->queue, 1u) : a.num_paths;
-                        if (!ABORT && nb >= a.num_paths && a.slice_q > 0) rb = ring_pop(a.rq, a.ring, a.ring_cap, epoch, ws);
+                        if (!ABORT && nb >= a.num_paths && a.slice_q > 0) rb = ring_pop(a.rq, a.ring, a.ring_cap, epoch, ws, a.num_paths, ring_wait_ticks(a.ring_test));
                     }
                 }
                 deq_hint = -1;
@@ -830,7 +912,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                                : (r == 30 ? pack2(__float_as_uint(t0), __float_as_uint(dt)) : pack2(w2, w3));
                         st_u64_h(a.susp + (size_t)b * SUSP_WORDS + r, word);
                         drain_stores();
-                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, epoch, b, hint >= 0, ws);
+                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, epoch, b, hint >= 0, ws, a.ring_test);
                         deq_hint = hint;
                         suspend = true;
                     } else if (hint == -1) {
@@ -1182,15 +1264,22 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
 
 // ---------------------------------------------------------------- host side
 static size_t ws_bytes_needed() { return (sizeof(Workspace) + 255) & ~(size_t)255; }
-// + the time-slicing area of a launch of `paths` paths: the ring counters, a
-// suspend block per path, then the ring
+// + the time-slicing area of a launch of `paths` paths: the ring counters, the
+// ring, then a suspend block per path.  The ring starts at a fixed offset, so
+// a workspace reused for launches of other sizes keeps its entry i at one
+// address (RQ_CLEARED counts entries from there); the suspend blocks follow
+// this launch's ring (256-B aligned) and may overwrite cleared entries past
+// it: k_prep_tables keeps that span as the dirty range (RQ_DLO, RQ_DHI) and
+// re-zeroes it when a later launch's ring covers it.
+static size_t ring_bytes(unsigned long long cap) { return ((size_t)cap * sizeof(unsigned long long) + 255) & ~(size_t)255; }
 static size_t ws_bytes_for(long long paths, int max_steps) {
     if (paths < 0) paths = 0;
     if (max_steps < 0) max_steps = 0;
-    return ws_bytes_needed() + ((RQ_WORDS * sizeof(unsigned) + (size_t)paths * SUSP_WORDS * sizeof(unsigned long long) +
-                                 (size_t)ring_entries(paths, max_steps) * sizeof(unsigned long long) + 255) &
-                                ~(size_t)255);
+    return ws_bytes_needed() + RQ_WORDS * sizeof(unsigned) + ring_bytes(ring_entries(paths, max_steps)) +
+           (size_t)paths * SUSP_WORDS * sizeof(unsigned long long);
 }
+// tests only (hc_trifocal_set_ring_test): pusher delay of every 16th ring ticket
+static int g_ring_test = 0;
 
 // Persistent grid: resident workgroups (occupancy API, cached per device and
 // kernel) x CUs, capped by the work.
@@ -1261,16 +1350,18 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
         ring_entries(paths, t->settings.max_steps) < 0xFFFFFF00ull &&
         slice_fits(t->settings.max_steps, t->settings.max_corrections, t->settings.delta_t_inc_steps)) {
         char *base = (char *)workspace + ws_bytes_needed();
-        k.rq = (unsigned *)base;
-        k.susp = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned));
-        k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) +
-                                        (size_t)paths * SUSP_WORDS * sizeof(unsigned long long));
         k.ring_cap = (unsigned)ring_entries(paths, t->settings.max_steps);
+        k.rq = (unsigned *)base;
+        k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned));
+        k.susp = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) + ring_bytes(k.ring_cap));
         k.slice_q = SLICE_Q;
+        k.ring_test = g_ring_test;
     }
     // control block reset, compacted tables (skipped when cached), ring reset
     PrepArgs pa{t->unified_index, ws, abort_mode ? ab->found_trifocal_sols : nullptr,
-                abort_mode ? ab->peer_found : nullptr, k.rq, k.ring, k.ring_cap};
+                abort_mode ? ab->peer_found : nullptr, k.rq, k.ring, k.ring_cap,
+                k.rq ? (unsigned)(ring_bytes(k.ring_cap) / 8) : 0u,
+                k.rq ? (unsigned)(ring_bytes(k.ring_cap) / 8 + (size_t)paths * SUSP_WORDS) : 0u};
     hipLaunchKernelGGL(k_prep_tables, dim3(1), dim3(PREP_THREADS), 0, s, pa);
     if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     // tracking: term tables read from the workspace (L1/L2), 96 VGPRs, 27.6 KB LDS
@@ -1416,7 +1507,7 @@ hcStatus hc_trifocal_eval_batched(int n, const int32_t *unified_index, const hcC
     hipStream_t s = (hipStream_t)stream;
     hc::Workspace *ws = (hc::Workspace *)workspace;
     (void)hipGetLastError();
-    hc::PrepArgs pa{unified_index, ws, nullptr, nullptr, nullptr, nullptr, 0u};
+    hc::PrepArgs pa{unified_index, ws, nullptr, nullptr, nullptr, nullptr, 0u, 0u, 0u};
     hipLaunchKernelGGL(hc::k_prep_tables, dim3(1), dim3(hc::PREP_THREADS), 0, s, pa);
     if (hc::launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     const int per = 2 * hc::WAVES_PER_WG;
@@ -1430,19 +1521,47 @@ const char *hc_last_error_string(void) { return hipGetErrorString(hc::g_last_hip
 
 static_assert(sizeof(hcIpcHandle) == sizeof(hipIpcMemHandle_t), "hcIpcHandle mirrors hipIpcMemHandle_t");
 
+namespace hc {
+// memory kind of each flag this process created (hc_shared_flag_memory_kind)
+static std::mutex g_flag_mu;
+static std::map<const void *, int> g_flag_kind;
+}  // namespace hc
+
+// The flag is polled by running kernels of other devices (system-scope loads
+// and stores over xGMI), so it is allocated where HIP specifies cross-agent
+// coherence while kernels run: uncached device memory first (every access
+// goes to the owner's memory), fine-grained memory next, plain
+// (coarse-grained, coherent only at synchronisation points) as the last
+// resort -- each only if it can be exported with hipIpcGetMemHandle.
 hcStatus hc_shared_flag_create(uint32_t **flag, hcIpcHandle *handle) {
     if (!flag || !handle) return HC_ERROR_INVALID_VALUE;
-    void *p = nullptr;
-    if ((hc::g_last_hip_error = hipMalloc(&p, 256)) != hipSuccess) return HC_ERROR_DEVICE;
-    hipIpcMemHandle_t h;
-    if ((hc::g_last_hip_error = hipMemset(p, 0, 256)) != hipSuccess ||
-        (hc::g_last_hip_error = hipIpcGetMemHandle(&h, p)) != hipSuccess) {
-        (void)hipFree(p);
-        return HC_ERROR_DEVICE;
+    static const unsigned kinds[3] = {hipDeviceMallocUncached, hipDeviceMallocFinegrained, hipDeviceMallocDefault};
+    hipError_t last = hipSuccess;
+    for (int k = 0; k < 3; k++) {
+        void *p = nullptr;
+        last = (kinds[k] == hipDeviceMallocDefault) ? hipMalloc(&p, 256) : hipExtMallocWithFlags(&p, 256, kinds[k]);
+        if (last != hipSuccess) { (void)hipGetLastError(); continue; }
+        hipIpcMemHandle_t h;
+        if ((last = hipMemset(p, 0, 256)) != hipSuccess || (last = hipDeviceSynchronize()) != hipSuccess ||
+            (last = hipIpcGetMemHandle(&h, p)) != hipSuccess) {
+            (void)hipGetLastError();
+            (void)hipFree(p);
+            continue;
+        }
+        memcpy(handle, &h, sizeof(h));
+        *flag = (uint32_t *)p;
+        std::lock_guard<std::mutex> g(hc::g_flag_mu);
+        hc::g_flag_kind[p] = 2 - k;
+        return HC_SUCCESS;
     }
-    memcpy(handle, &h, sizeof(h));
-    *flag = (uint32_t *)p;
-    return HC_SUCCESS;
+    hc::g_last_hip_error = last;
+    return HC_ERROR_DEVICE;
+}
+
+int hc_shared_flag_memory_kind(const uint32_t *flag) {
+    std::lock_guard<std::mutex> g(hc::g_flag_mu);
+    const auto it = hc::g_flag_kind.find(flag);
+    return it == hc::g_flag_kind.end() ? -1 : it->second;
 }
 
 hcStatus hc_shared_flag_open(const hcIpcHandle *handle, uint32_t **flag) {
@@ -1465,6 +1584,10 @@ hcStatus hc_shared_flag_reset(uint32_t *flag, hcStream stream) {
 
 hcStatus hc_shared_flag_close(uint32_t *flag, int opened) {
     if (!flag) return HC_ERROR_INVALID_VALUE;
+    if (!opened) {
+        std::lock_guard<std::mutex> g(hc::g_flag_mu);
+        hc::g_flag_kind.erase(flag);
+    }
     hc::g_last_hip_error = opened ? hipIpcCloseMemHandle(flag) : hipFree(flag);
     return hc::g_last_hip_error == hipSuccess ? HC_SUCCESS : HC_ERROR_DEVICE;
 }
@@ -1491,8 +1614,12 @@ int hc_diag_util(unsigned long long *out, int reset) {
 }
 #endif
 
+int hc_trifocal_abi_version(void) { return HC_TRIFOCAL_ABI_VERSION; }
+
+void hc_trifocal_set_ring_test(int delay_ticks) { hc::g_ring_test = delay_ticks > 0 ? delay_ticks : 0; }
+
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.3 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
+    return "hc_trifocal gfx950 v9.4 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
            "readlane back substitution, pipelined evals with entry-grouped dH/dx terms, 5 waves/SIMD, time slicing "
            "at step boundaries with least-attained-service issue priority)";
 }

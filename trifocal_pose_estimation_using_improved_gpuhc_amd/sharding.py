@@ -198,21 +198,36 @@ class SharedFlag:
         self._rank = rank
 
     def arm(self, stream=None) -> None:
-        """Zeroes the flag before a run: the owner resets and synchronises, then
-        all ranks pass a barrier, so no launch starts before the reset."""
+        """Zeroes the flag before a run.  Every rank first drains its device
+        (a launch of the previous run still queued on a non-owner rank could
+        otherwise set the flag after the reset), then the owner resets and
+        synchronises, and a barrier on both sides orders the reset after every
+        rank's previous launches and before any rank's next one."""
         import ctypes as C
 
         import torch
         import torch.distributed as dist
         if self.ptr is None:
             return
+        s = stream if stream is not None else torch.cuda.current_stream()
+        torch.cuda.synchronize(s.device)
+        dist.barrier(group=self._group)
         if self._rank == self._owner:
-            s = stream if stream is not None else torch.cuda.current_stream()
             st = self._L.hc_shared_flag_reset(C.c_void_p(self.ptr), C.c_void_p(s.cuda_stream))
             if st != 0:
                 raise RuntimeError(f"hc_shared_flag_reset failed: {st}")
             s.synchronize()
         dist.barrier(group=self._group)
+
+    @property
+    def memory_kind(self):
+        """The owner's allocation (include/hc_trifocal.h hc_shared_flag_memory_kind):
+        'uncached', 'fine-grained', 'coarse-grained', or None on a mapping rank."""
+        import ctypes as C
+        if self.ptr is None or self._rank != self._owner:
+            return None
+        k = self._L.hc_shared_flag_memory_kind(C.c_void_p(self.ptr))
+        return {2: "uncached", 1: "fine-grained", 0: "coarse-grained"}.get(k)
 
     def close(self) -> None:
         """Collective: the mapping ranks unmap before the owner frees."""
