@@ -34,7 +34,8 @@ def main():
     L = _abi.lib()
     fn = L.hc_diag_luwork
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    out = (C.c_ulonglong * 3)()
+    fn.restype = C.c_int
+    out = (C.c_ulonglong * 10)()
     dev = torch.device("cuda:0")
     problem = load_problem()
     tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, 100)
@@ -46,13 +47,17 @@ def main():
     r = tr.allocate(tgt.shape[0])
     tr.reset_tracks(r)
     torch.cuda.synchronize()
-    fn(out, 1)
+    if fn(out, 1) != 0:
+        raise RuntimeError("hc_diag_luwork failed (a diagnostic build of other sources?)")
     tr.launch(torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev), r)
     torch.cuda.synchronize()
-    fn(out, 1)
+    if fn(out, 1) != 0:
+        raise RuntimeError("hc_diag_luwork failed")
     st = r.stats.cpu().numpy()
     stages = 4 * int(st[:, 0].sum()) + int(st[:, 1].sum())
     elems, solves, dense = int(out[0]), int(out[1]), int(out[2])
+    wsolves, groups, rare = int(out[3]), int(out[4]), int(out[5])
+    ev = [int(out[6]), int(out[7]), int(out[8])]
     res = {"config": ("sample 0 of config 2 + its target params x 2^40, x 2^70 (one launch)" if scaled
                       else "config 2 (100 samples, abort off), one launch"),
            "sparse_solves_completed": solves, "path_stages": stages,
@@ -63,6 +68,13 @@ def main():
            "executed_update_elements_per_solve": elems / max(1, solves),
            "dense_update_elements_per_solve": DENSE_UPDATE_ELEMENTS,
            "executed_fraction": elems / max(1, solves) / DENSE_UPDATE_ELEMENTS,
+           "wave_solves": wsolves,
+           "live_groups_per_wave_solve": groups / max(1, wsolves),
+           "rare_steps_per_wave_solve": rare / max(1, wsolves),
+           "wave_stages": sum(ev),
+           "rhs_eval_kinds": {"mixed": ev[0], "dHdt_only": ev[1], "H_only": ev[2]},
+           "prefix_rebuilds": int(out[9]),
+           "prefix_rebuilds_per_wave_stage": int(out[9]) / max(1, sum(ev)),
            # the product build of the same sources (bench.py prices its LU with this file)
            "build_id": _abi.build_id(_abi.PRODUCT_LIB_PATH),
            "diag_build_id": _abi.build_id(),

@@ -151,9 +151,9 @@ def _rank_main_shared_flag(rank, world, port, out_dir):
         parts = tr.launch_abort_chunked(t, d, r, cnt, wss, stream=stream, inflight_stop=True, peer_found=flag)
         torch.cuda.synchronize(dev)
         h = r.host()
+        kind = flag.memory_kind
         dist.barrier()
         flag.close()
-        kind = flag.memory_kind
         np.savez(os.path.join(out_dir, f"rank{rank}.npz"), off=off, cnt=cnt, nchunks=len(parts),
                  tracks=h["tracks"], conv=h["converge"], steps=h["stats"]["steps"],
                  batch_index=h["batch_index"], found=h["found"], kind=str(kind))

@@ -263,11 +263,13 @@ def test_time_slicing_falls_back_when_the_ring_does_not_fit(problem, samples100,
 
 
 def test_time_slicing_workspace_reused_across_launch_sizes(problem, samples100, tracker):
-    """One workspace, sliced launches of 100, then 3, then 100 samples: the
-    ring sits at a fixed offset, so the 3-sample launch meets only entries
+    """One workspace, sliced launches of 100, then 50, then 100 samples: the
+    ring sits at a fixed offset, so the 50-sample launch meets only entries
     tagged by an older epoch; its suspend blocks follow its ring and overwrite
     cleared entries, which it records as the dirty range, and the second
-    100-sample launch re-zeroes them.  Every launch equals the serial run bit for bit."""
+    100-sample launch re-zeroes them.  (50 samples: 15 600 paths,
+    more than the 10 240 path slots of a full grid, so that launch suspends
+    paths too.)  Every launch equals the serial run bit for bit."""
     import torch
     tgt, dif, _ = samples100
     ref = tracker.track(tgt, dif, time_slicing=False).host()
@@ -275,7 +277,7 @@ def test_time_slicing_workspace_reused_across_launch_sizes(problem, samples100, 
     t, d = torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev)
     ws = tracker.new_workspace(100)
     off = int(tracker.L.hc_trifocal_workspace_size())
-    for n in (100, 3, 100):
+    for n in (100, 50, 100):
         r = tracker.allocate(n)
         tracker.reset_tracks(r)
         tracker.launch(t, d, r, workspace=ws, num_samples=n)
@@ -284,11 +286,11 @@ def test_time_slicing_workspace_reused_across_launch_sizes(problem, samples100, 
         rq = np.frombuffer(ws[off:off + 1024].cpu().numpy().tobytes(), np.uint32)
         assert rq[64] > 0 and rq[0] == rq[64], "sliced, and every suspended path resumed"
         # RQ_CLEARED: the largest ring so far (one entry per possible suspension + 4096 spare);
-        # after the 3-sample launch its suspend blocks lie inside it: the dirty range [195, 196)
+        # after the 50-sample launch its suspend blocks lie inside it: the dirty range [195, 196)
         cap = lambda k: k * 312 * ((tracker.settings.max_steps + 1) // 3 + 1) + 4096  # noqa: E731
         assert rq[194] == cap(100)
-        if n == 3:
-            assert cap(3) <= rq[195] < rq[196] <= cap(100)
+        if n == 50:
+            assert cap(50) <= rq[195] < rq[196] <= cap(100)
         else:
             assert rq[195] == rq[196] == 0
         h = r.host()
@@ -304,10 +306,11 @@ def test_time_slicing_abandoned_tickets_are_pushed_again(problem, samples100, tr
     (VERDICT r3 #5).  hc_trifocal_set_ring_test delays every 16th ticket's
     entry by 2 ms and lets consumers abandon after 250 us; the launch abandons
     tickets (control block word 12) and still equals the unsliced run bit for
-    bit, with no device error."""
+    bit, with no device error.  (50 samples: more paths than path slots, so
+    paths are suspended.)"""
     import torch
     tgt, dif, _ = samples100
-    n = 20
+    n = 50
     ref = tracker.track(tgt[:n], dif[:n], time_slicing=False).host()
     dev = tracker.device
     ws = tracker.new_workspace(n)

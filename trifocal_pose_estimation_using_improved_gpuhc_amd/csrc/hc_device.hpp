@@ -65,6 +65,17 @@ __device__ __forceinline__ cf cdiv_apply(cf x, const divf &f) {
     return cmk(((ars * f.brs) + (ais * f.bis)) * f.o2, ((ais * f.brs) - (ars * f.bis)) * f.o2);
 }
 
+// Phase markers of the HC_DIAG_ISA build (scripts/isa_phases.py): assembly
+// comments that split the tracker's ISA into the phases of a stage.  Empty in
+// every other build.
+#ifdef HC_DIAG_ISA
+#define HC_ISA_MARK(name) asm volatile(";HCPH " name)
+#define HC_ISA_MARK_I(name, i) asm volatile(";HCPH " name " %0" ::"i"(i))
+#else
+#define HC_ISA_MARK(name) do { } while (0)
+#define HC_ISA_MARK_I(name, i) do { } while (0)
+#endif
+
 // ------------------------------------------------------------------ lanes
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 // The lane id computed where it is used (v_mbcnt on an opaque all-ones mask):

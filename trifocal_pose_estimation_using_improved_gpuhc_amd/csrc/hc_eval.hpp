@@ -6,8 +6,16 @@
 // evaluates equation row r of its path from compacted per-row term lists:
 //
 //  * term words carry LDS byte offsets relative to the path slot (SlotLDS), so
-//    an operand address is one add (p offsets in 16-bit halves, x offsets in
-//    bytes) instead of shift + mask + add;
+//    an operand address is one add (prefix offsets in 16-bit halves, x
+//    offsets in bytes) instead of shift + mask + add;
+//  * prefix tables (round 4): a term's parameter part depends only on its
+//    (coef, a, b) -- (c * p[a]) * p[b] for dH/dx and H, c * (d[a]*p[b] +
+//    d[b]*p[a]) for dH/dt -- and p(t) changes only with t, so each slot keeps
+//    the 93 distinct (c * p[a]) * p[b] and the 38 distinct d[a]*p[b] +
+//    d[b]*p[a] of this problem in LDS (SlotLDS::tp, qp), rebuilt by
+//    build_prefixes when its t or sample changes (about 0.4 times per stage),
+//    and a term reads its prefix instead of two or four parameters: the same
+//    operations on the same values, so the results are bit-identical;
 //  * the complex products use packed FP32 (v_pk_mul_f32 / v_pk_fma_f32): two
 //    instructions per complex multiply / multiply-add, each component computed
 //    by the same fma chain as the scalar spec;
@@ -56,29 +64,40 @@ __host__ __device__ constexpr int hx_gslot(int k) {
 }
 static_assert(hx_gend(5) == HX_SLOT_CAP, "slot capacities");
 constexpr int SLOT_OFF_X = (int)offsetof(SlotLDS, x);
-constexpr int SLOT_OFF_P = (int)offsetof(SlotLDS, p);
-constexpr int SLOT_DIF_DELTA = (int)offsetof(SlotLDS, dif) - (int)offsetof(SlotLDS, p);
 constexpr int SLOT_OFF_ENT = (int)offsetof(SlotLDS, ent);
-constexpr int SLOT_OFF_HXDUMMY = (int)offsetof(SlotLDS, lu) + 8 * 31;   // unused entry slots store here
-static_assert(SLOT_OFF_ENT + 8 * NV * 7 < 65536 && SLOT_OFF_HXDUMMY < 65536, "entry offsets must fit 16 bits");
+constexpr int SLOT_OFF_ENTZERO = SLOT_OFF_ENT + 8 * (ENT_CAP - 1);        // the structural zero
+// while the prefixes are built, p(t) is staged in ent[0..33] and the diff
+// params in ent[34..67] (the entries are rewritten by the stage's dH/dx)
+constexpr int SLOT_OFF_STG = SLOT_OFF_ENT;
+constexpr int SLOT_STG_DIF_DELTA = 8 * NPP;
+constexpr int SLOT_OFF_TP = (int)offsetof(SlotLDS, tp);
+constexpr int SLOT_OFF_QP = (int)offsetof(SlotLDS, qp);
+constexpr int SLOT_OFF_HXDUMMY = (int)offsetof(SlotLDS, lu) + 8 * 31;   // unused entry / prefix slots store here
+static_assert(SLOT_OFF_QP + 8 * QP_CAP < 65536 && SLOT_OFF_HXDUMMY < 65536, "slot offsets must fit 16 bits");
 static_assert(SLOT_OFF_X + 8 * 31 < 256, "x offsets must fit a byte");
-static_assert(SLOT_OFF_P + 8 * NPP < 65536, "p offsets must fit 16 bits");
+static_assert(2 * NPP <= ENT_CAP - 1, "the staging area lies below the structural zero");
 
-// Compacted tables, built once per launch by k_prep_tables from the
-// reference's padded unified index (Data_Reader.cpp:167-189).
-//  map[q][r]  (row r): column c -> entry slot of row r's block in SlotLDS::ent
-//             (3 bits x 10 columns per word, 6 = structural zero)
-//  hx[k][l] (lane l's k-th dH/dx term, entry slot hx_gslot(k)): .x = off(p[a]) | off(p[b]) << 16
-//                                      .y = off(x[u]) | off(x[v]) << 8 | (int8)coef << 16
+// Compacted tables, built by k_prep_tables from the reference's padded
+// unified index (Data_Reader.cpp:167-189) and kept in the workspace.
+//  gm[q][r]   (row r): SlotLDS byte offsets of row r's entries in columns 2q
+//             (bits 0..15) and 2q+1 (bits 16..31); the structural zero for
+//             columns without terms
+//  pat[r]     structural pattern of row r (bit c: column c has terms)
+//  hx[k][l]   (lane l's k-th dH/dx term, entry slot hx_gslot(k)):
+//             off(tp[i]) | off(x[u]) << 16 | off(x[v]) << 24, i = its (c, a, b)
 //  hxd[q][l]  (lane l): SlotLDS byte offsets its slots 2q (bits 0..15) and 2q+1 (bits 16..31) store to
-//  ht[j][r] (row r's j-th dH/dt / H term): .x = off(p[a]) | off(p[b]) << 16
-//                                      .y = off(x[u]) | off(x[v]) << 8 | off(x[w]) << 16 | (int8)coef << 24
-// (float)(int8_t)(w.y >> 16) in one SDWA convert (the compiler's form took a
-// v_alignbit first); the dH/dt | H coefficient is the top byte.  (Float
-// coefficients in 12-byte term words measured no faster: profiles/r3p_*.)
-__device__ __forceinline__ float coef_hx(const uint2 &w) {
+//  ht[j][r]   (row r's j-th dH/dt / H term): .x = off(tp[i]) | off(qp[m]) << 16, i its (c, a, b), m its (a, b)
+//                                            .y = off(x[u]) | off(x[v]) << 8 | off(x[w]) << 16 | (int8)coef << 24
+//  pre[k][l]  build_prefixes' job of lane l in round k (rounds 0..2: tp, 3..4: qp):
+//             .x = off(p[a]) | off(p[b]) << 16 in the staging area, .y = destination | (int8)coef << 16
+//             (padding jobs: a = b = 33, coef 0, destination SLOT_OFF_HXDUMMY)
+constexpr int GM_WORDS = NV / 2;
+constexpr int PRE_TP_ROUNDS = (TP_CAP + 31) / 32, PRE_ROUNDS = PRE_TP_ROUNDS + (QP_CAP + 31) / 32;
+// the coefficient in byte 2 of a word, in one SDWA convert (the compiler's
+// form took a v_alignbit first)
+__device__ __forceinline__ float coef_b2(uint32_t w) {
     float co;
-    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(co) : "v"(w.y));
+    asm("v_cvt_f32_i32_sdwa %0, sext(%1) dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2" : "=v"(co) : "v"(w));
     return co;
 }
 __device__ __forceinline__ float coef_ht(const uint2 &w) { return (float)((int)w.y >> 24); }
@@ -89,11 +108,13 @@ struct EvalTables {
     unsigned pad;
     unsigned long long src_hash;      // hash of the unified index they were built from
     unsigned long long pad2;
-    uint32_t map[3][32];
+    uint32_t gm[GM_WORDS][32];
+    uint32_t pat[32];
     uint32_t hxd[HX_NSLOT / 2][32];
     uint32_t ht_acc_mask[4];          // eval_rhs: lanes (of a half) that accumulate in help term q
     uint32_t ht_light_mask[4];        // eval_rhs: lanes that accumulate a helper's product in light term q
-    uint2 hx[HX_SLOT_CAP * 32];
+    uint2 pre[PRE_ROUNDS][32];
+    uint32_t hx[HX_SLOT_CAP * 32];
     uint2 ht[HT_TERMS * 32];
 };
 
@@ -131,20 +152,23 @@ __device__ __forceinline__ pf2 pcmsub(pf2 acc, pf2 a, pf2 b) {
 // ahead of the previous terms' entry stores (which the compiler may not move
 // loads across), so a lane has several terms' LDS reads in flight instead of
 // one round trip per term, with few registers held.
-constexpr int EV_AHEAD = 2;
+#ifndef HC_EV_AHEAD
+#define HC_EV_AHEAD 2
+#endif
+constexpr int EV_AHEAD = HC_EV_AHEAD;
 constexpr int EV_WAHEAD = EV_AHEAD + 2;
 
-struct HxOps { pf2 pa, pb, xu, xv; };
-template <typename TW>
-__device__ __forceinline__ HxOps hx_ops(const char *sb, const TW &w) {
-    return HxOps{ldp(sb, w.x & 0xFFFFu), ldp(sb, w.x >> 16), ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu)};
+struct HxOps { pf2 t, xu, xv; };
+__device__ __forceinline__ HxOps hx_ops(const char *sb, uint32_t w) {
+    return HxOps{ldp(sb, w & 0xFFFFu), ldp(sb, (w >> 16) & 0xFFu), ldp(sb, w >> 24)};
 }
 
-// the term loop of eval_hx: operands are read through sb (x, p of the slot),
-// each finished entry is stored at sb + the lane's destination offset
-template <typename TW>
-__device__ __forceinline__ void eval_hx_terms(const TW *s_hx, const uint32_t *s_hxd, char *sb, int r) {
-    TW w[HX_SLOT_CAP];
+// the term loop of eval_hx: operands are read through sb (the slot's prefix
+// table tp and x), each finished entry is stored at sb + the lane's
+// destination offset.  A term is ((c * p[a]) * p[b]) * x[u] accumulated with
+// x[v] (:57-88); its prefix (c * p[a]) * p[b] comes from tp (build_prefixes).
+__device__ __forceinline__ void eval_hx_terms(const uint32_t *s_hx, const uint32_t *s_hxd, char *sb, int r) {
+    uint32_t w[HX_SLOT_CAP];
     uint32_t dst[HX_NSLOT / 2];
 #pragma unroll
     for (int q = 0; q < HX_NSLOT / 2; q++) dst[q] = s_hxd[q * 32 + r];
@@ -159,10 +183,7 @@ __device__ __forceinline__ void eval_hx_terms(const TW *s_hx, const uint32_t *s_
         if (k + EV_WAHEAD < HX_SLOT_CAP) w[k + EV_WAHEAD] = s_hx[(k + EV_WAHEAD) * 32 + r];
         if (k + EV_AHEAD < HX_SLOT_CAP) o[(k + EV_AHEAD) % (EV_AHEAD + 1)] = hx_ops(sb, w[k + EV_AHEAD]);
         const HxOps &q = o[k % (EV_AHEAD + 1)];
-        const float co = coef_hx(w[k]);
-        pf2 P = q.pa * pf2{co, co};
-        P = pcmul(P, q.pb);
-        P = pcmul(P, q.xu);
+        const pf2 P = pcmul(q.t, q.xu);
         acc = pcmadd(acc, P, q.xv);
         if (hx_is_gend(k)) {                 // static: the entry in slot hx_gslot(k) ends here on every lane
             const int sl = hx_gslot(k);
@@ -177,25 +198,12 @@ __device__ __forceinline__ void eval_hx_terms(const TW *s_hx, const uint32_t *s_
 // dH/dx: row r of both paths' Jacobians into rA.  The term loop is fully
 // unrolled over the padded table (HX_SLOT_CAP words per lane) and branch-free,
 // so several terms' LDS reads stay in flight; each entry slot is stored once,
-// where its group of terms ends, slot 6 (structural zero) is zeroed, and 30
-// gathers through the column -> slot map rebuild the register row.
-// the register row r of dH/dx from the lane's entry block (S.ent row r)
-// The gather map of row r: half c % 2 of word c / 2 = the SlotLDS byte
-// offset of column c's entry (its entry slot in row r's block of
-// SlotLDS::ent; slot 6: the structural zero), so a gather address is one
-// SDWA add, as the evaluations' operand addresses (a 3-bit slot code took a
-// v_bfe and a v_lshl_add).  Built once per launch; its 15 words are read from
-// LDS (stride 32 words) where the gather runs.
-constexpr int GM_WORDS = NV / 2;
-__device__ __forceinline__ uint32_t gather_map_word(const uint32_t (&map)[3], int r, int q) {
-    uint32_t v = 0;
-    for (int k = 0; k < 2; k++) {
-        const int c = 2 * q + k;
-        const uint32_t code = (map[c / 10] >> (3 * (c % 10))) & 7u;
-        v |= ((uint32_t)SLOT_OFF_ENT + 8u * ((uint32_t)(r < NV ? r : 0) * 7u + code)) << (16 * k);
-    }
-    return v;
-}
+// where its group of terms ends, and 30 gathers through the row's gather map
+// rebuild the register row.  The gather map of row r (EvalTables::gm): half c %
+// 2 of word c / 2 = the SlotLDS byte offset of column c's entry in the packed
+// entry block (or of the structural zero), so a gather address is one SDWA
+// add, as the evaluations' operand addresses.  Its 15 words are read from LDS
+// (stride 32 words) where the gather runs.
 __device__ __forceinline__ void gather_hx(cf (&rA)[NV], const uint32_t *gmw, const SlotLDS &S, int r) {
     const char *sb = reinterpret_cast<const char *>(&S);
     uint32_t g[GM_WORDS];
@@ -208,29 +216,67 @@ __device__ __forceinline__ void gather_hx(cf (&rA)[NV], const uint32_t *gmw, con
     }
 }
 
-template <typename TW>
-__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const TW *s_hx, const uint32_t *s_hxd,
+__device__ __forceinline__ void eval_hx(cf (&rA)[NV], const uint32_t *s_hx, const uint32_t *s_hxd,
                                         const uint32_t *gmw, SlotLDS &S, int r) {
-    cf *ent_row = S.ent + (r < NV ? r : 0) * 7;
     eval_hx_terms(s_hx, s_hxd, reinterpret_cast<char *>(&S), r);
-    float z;   // a fresh zero (a hoisted zero pair gets spilled in abort mode)
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    if (r < NV) ent_row[6] = cmk(z, z);   // structural zero
     wave_lds_sync();
+    HC_ISA_MARK("ev_gather");
     gather_hx(rA, gmw, S, r);
 }
 
-struct HtOps { pf2 pa, pb, da, db, xu, xv, xw; };
-template <typename TW>
-__device__ __forceinline__ HtOps ht_ops(const char *sb, const TW &w) {
-    const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
-    return HtOps{ldp(sb, oa), ldp(sb, ob), ldp(sb + SLOT_DIF_DELTA, oa), ldp(sb + SLOT_DIF_DELTA, ob),
-                 ldp(sb, w.y & 0xFFu), ldp(sb, (w.y >> 8) & 0xFFu), ldp(sb, (w.y >> 16) & 0xFFu)};
+// The slot's prefix tables (round 4).  p and the diff params are staged in
+// the entry block (ent[0..33], ent[34..67]), then every lane runs its jobs
+// (EvalTables::pre): (c * p[a]) * p[b] into tp and d[a]*p[b] + d[b]*p[a] into
+// qp, with the operations of the term loops they replace (:57-148).  The two
+// halves build their own slots' tables in the same instructions.
+template <typename PW>
+__device__ __forceinline__ void build_prefix_rounds(SlotLDS &S, int r, const PW *pre) {
+    char *sb = reinterpret_cast<char *>(&S);
+    wave_lds_sync();
+#pragma unroll
+    for (int k = 0; k < PRE_TP_ROUNDS; k++) {
+        const uint2 w = pre[k * 32 + r];
+        const pf2 pa = ldp(sb, w.x & 0xFFFFu), pb = ldp(sb, w.x >> 16);
+        const float co = coef_b2(w.y);
+        const pf2 t = pcmul(pa * pf2{co, co}, pb);                                     // (c * p[a]) * p[b]
+        *reinterpret_cast<pf2 *>(sb + (w.y & 0xFFFFu)) = t;
+    }
+#pragma unroll
+    for (int k = PRE_TP_ROUNDS; k < PRE_ROUNDS; k++) {
+        const uint2 w = pre[k * 32 + r];
+        const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
+        const pf2 pa = ldp(sb, oa), pb = ldp(sb, ob);
+        const pf2 da = ldp(sb + SLOT_STG_DIF_DELTA, oa), db = ldp(sb + SLOT_STG_DIF_DELTA, ob);
+        const pf2 q = pcmadd(pcmul(da, pb), db, pa);                                   // d[a]*p[b] + d[b]*p[a]
+        *reinterpret_cast<pf2 *>(sb + (w.y & 0xFFFFu)) = q;
+    }
+    wave_lds_sync();
+}
+// The tracker's: lane r stages p[r] = t * target[r] + (1 - t) * start[r] (lane
+// 0 also p[32]; p[33] = 1; ..._TrunPaths.cu:181 via the p(t) helper of
+// dev-eval-indxing-..._LimUnroll_L2Cache.cuh:40-54) and d[r] from the slot's
+// sample (global memory, L2-resident); sp: the start params (LDS).
+template <typename PW>
+__device__ __forceinline__ void build_prefixes(SlotLDS &S, int r, const PW *pre, const cf *target, const cf *diff,
+                                               const cf *sp, float t0) {
+    cf *stg = S.ent;
+    const float omt = (float)(1.0 - (double)t0);
+    stg[r] = cadd(cscale(target[r], t0), cscale(sp[r], omt));
+    stg[NPP + r] = diff[r];
+    if (r == 0) {
+        stg[32] = cadd(cscale(target[32], t0), cscale(sp[32], omt));
+        stg[33] = cmk(1.0f, 0.0f);
+        stg[NPP + 32] = diff[32];
+        stg[NPP + 33] = diff[33];
+    }
+    build_prefix_rounds(S, r, pre);
 }
 
 // dH/dt, H and the merged pass share one loop (eval_rhs).
-//  * dH/dt: b = -sum_j c*(d[a]*p[b] + d[b]*p[a])*x[u]*x[v]*x[w]  (:91-119)
-//  * H:     b =  sum_j c*p[a]*p[b]*x[u]*x[v]*x[w]               (:122-148)
+//  * dH/dt: b = -sum_j c*(d[a]*p[b] + d[b]*p[a])*x[u]*x[v]*x[w]  (:91-119),
+//    d[a]*p[b] + d[b]*p[a] from the slot's qp table;
+//  * H:     b =  sum_j c*p[a]*p[b]*x[u]*x[v]*x[w]               (:122-148),
+//    (c*p[a])*p[b] from the slot's tp table (build_prefixes);
 //  * merged (RHS_MIXED): dH/dt in the halves with ht_half, H in the others, in
 //    one pass, for a wave whose two paths run different stage kinds
 //    (predictor | corrector: 44 % of the wave-stages of config 2) instead of
@@ -302,17 +348,12 @@ __device__ __forceinline__ RhsMasks rhs_masks(const EvalTables *T) {
 }
 
 template <int KIND>
-struct RhsOps { pf2 pa, pb, da, db, xu, xv, xw; };
+struct RhsOps { pf2 t, q, xu, xv, xw; };
 template <int KIND, typename TW>
 __device__ __forceinline__ RhsOps<KIND> rhs_ops(const char *sb, const TW &w) {
-    const uint32_t oa = w.x & 0xFFFFu, ob = w.x >> 16;
     RhsOps<KIND> o;
-    o.pa = ldp(sb, oa);
-    o.pb = ldp(sb, ob);
-    if constexpr (KIND != RHS_H) {
-        o.da = ldp(sb + SLOT_DIF_DELTA, oa);
-        o.db = ldp(sb + SLOT_DIF_DELTA, ob);
-    }
+    if constexpr (KIND != RHS_HT) o.t = ldp(sb, w.x & 0xFFFFu);     // (c * p[a]) * p[b]
+    if constexpr (KIND != RHS_H) o.q = ldp(sb, w.x >> 16);          // d[a]*p[b] + d[b]*p[a]
     o.xu = ldp(sb, w.y & 0xFFu);
     o.xv = ldp(sb, (w.y >> 8) & 0xFFu);
     o.xw = ldp(sb, (w.y >> 16) & 0xFFu);
@@ -339,17 +380,13 @@ __device__ __forceinline__ cf eval_rhs(const TW *s_ht, const SlotLDS &S, int r, 
         const float co = coef_ht(w[j]);
         pf2 P;
         if constexpr (KIND == RHS_HT) {
-            pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
-            s = s * pf2{co, co};
+            const pf2 s = q.q * pf2{co, co};
             P = pcmul(pcmul(s, q.xu), q.xv);
         } else if constexpr (KIND == RHS_H) {
-            P = q.pa * pf2{co, co};
-            P = pcmul(pcmul(pcmul(P, q.pb), q.xu), q.xv);
+            P = pcmul(pcmul(q.t, q.xu), q.xv);
         } else {
-            pf2 s = pcmadd(pcmul(q.da, q.pb), q.db, q.pa);
-            s = s * pf2{-co, -co};
-            const pf2 h = pcmul(q.pa * pf2{co, co}, q.pb);
-            const pf2 pre = {ht_half ? s.x : h.x, ht_half ? s.y : h.y};
+            const pf2 s = q.q * pf2{-co, -co};
+            const pf2 pre = {ht_half ? s.x : q.t.x, ht_half ? s.y : q.t.y};
             P = pcmul(pcmul(pre, q.xu), q.xv);
         }
         if (j < HT_HELP_FIRST) {

@@ -222,10 +222,13 @@ __device__ __forceinline__ unsigned long long xchg_u64(unsigned long long *p, un
 // Publishes suspended path b (its block already written and drained).  A
 // pusher that finds its ticket abandoned -- it was paused between taking the
 // ticket and writing the entry for longer than the consumer waits -- pushes
-// again on a new ticket, as an unpaired entry: the consumer of the abandoned
-// ticket looks for a path with an unpaired pop (ring_pop), so this entry must
-// be claimable.  test_delay (tests only): every 16th ticket waits that many
-// ticks before its exchange, so that its consumer abandons it.
+// again on a new ticket, paired or unpaired as before.  Accounting: every
+// live entry is matched by one pop, either a claim on avail (unpaired
+// entries publish one) or the paired pop its pusher makes next; an abandoned
+// ticket takes one pop with it, and its consumer restores the balance
+// (ring_pop gives its claim back; ring_pop_paired publishes its own paired
+// push as claimable).  test_delay (tests only): every 16th ticket waits that
+// many ticks before its exchange, so that its consumer abandons it.
 __device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch, int b,
                                           bool unpaired, Workspace *ws, int test_delay) {
     for (;;) {
@@ -241,7 +244,6 @@ __device__ __forceinline__ void ring_push(unsigned *rq, unsigned long long *ring
         const unsigned tag = ring_tag(epoch, t);
         const unsigned long long old = xchg_u64(&ring[t], ((unsigned long long)tag << 32) | (unsigned)b);
         if (__builtin_expect(old != ring_abandon_mark(tag), 1)) break;
-        unpaired = true;
     }
     if (unpaired) atomicAdd(&rq[RQ_AVAIL], 1u);
 }
@@ -304,12 +306,16 @@ __device__ __forceinline__ int ring_pop(unsigned *rq, unsigned long long *ring, 
     }
     return -1;
 }
-// the swap's pop, right after its own push (no claim); an abandoned ticket
-// falls back to an unpaired pop
+// the swap's pop, right after its own push (no claim).  If its ticket is
+// abandoned, the swap's own push has lost the pop that matched it: it is
+// published as claimable (avail), and the half looks for a path with an
+// unpaired pop
 __device__ __forceinline__ int ring_pop_paired(unsigned *rq, unsigned long long *ring, unsigned cap, unsigned epoch,
                                                Workspace *ws, int num_paths, unsigned long long wait_ticks) {
     const int b = ring_take(ring, cap, epoch, ws, atomicAdd(&rq[RQ_HEAD], 1u), rq, num_paths, wait_ticks);
-    return b != -2 ? b : ring_pop(rq, ring, cap, epoch, ws, num_paths, wait_ticks);
+    if (b != -2) return b;
+    atomicAdd(&rq[RQ_AVAIL], 1u);
+    return ring_pop(rq, ring, cap, epoch, ws, num_paths, wait_ticks);
 }
 
 // ---------------------------------------------------------------- table prep
@@ -417,18 +423,22 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
     }
     if (s_valid) return;   // tables built from this index table already
     const int r = tid;
-    const uint2 pad_hx = make_uint2((uint32_t)(SLOT_OFF_P + 8 * 33) | ((uint32_t)(SLOT_OFF_P + 8 * 33) << 16),
-                                    (uint32_t)(SLOT_OFF_X + 8 * 30) | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 8));
     // dH/dx: entries bin-packed over the 32 lanes (hc_eval.hpp).  A: terms per
     // entry (rows in parallel); B: one thread places the entries, largest first,
     // each in the smallest-capacity slot class with a free lane (ties: lower
-    // row, then lower column), numbering each row's entries 0..5 in placement
-    // order; C: rows write their entries' term words at their places.
+    // row, then lower column), numbering the entries 0..169 in placement order
+    // (their place in the slot's packed entry block), and lists the distinct
+    // prefix triples (c, a, b) of the dH/dx and H terms and pairs (a, b) of the
+    // dH/dt terms (padding first: (0, 33, 33) and (33, 33)); C: rows write their
+    // terms' words; D: the prefix build jobs.
     __shared__ uint8_t s_cnt[NV][NV];
     __shared__ int s_htn[32];             // dH/dt | H terms of row r (0 for lanes 30, 31)
     __shared__ uint8_t s_place[NV][NV];   // lane << 3 | slot, 0xFF: structural zero
-    __shared__ uint32_t s_map[3][32];
+    __shared__ uint16_t s_eoff[NV][NV];   // SlotLDS byte offset of entry (row, column)
     __shared__ uint32_t s_dst[HX_NSLOT / 2][32];
+    __shared__ uint32_t s_tri[TP_CAP];    // (uint8)c | a << 8 | b << 16
+    __shared__ uint32_t s_pair[QP_CAP];   // a | b << 8
+    __shared__ int s_ntri, s_npair;
     // slot capacities and starts as locals (a runtime index into the
     // namespace-scope constexpr table does not reach device memory)
     int cap[HX_NSLOT], start[HX_NSLOT];
@@ -438,6 +448,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         start[s2] = acc2;
         acc2 += cap[s2];
     }
+    const int32_t *D = U + HX_SIZE;
     if (r < NV)
         for (int c = 0; c < NV; c++) {
             int n = 0;
@@ -445,32 +456,30 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                 if (U[(c * HX_TERMS + j) * HX_PARTS * NV + r] != 0) n++;
             s_cnt[r][c] = (uint8_t)n;
             s_place[r][c] = 0xFFu;
+            s_eoff[r][c] = (uint16_t)SLOT_OFF_ENTZERO;
         }
     if (r < 32) {
-        for (int k2 = 0; k2 < HX_SLOT_CAP; k2++) T->hx[k2 * 32 + r] = pad_hx;
+        // padding words first (other lanes' rows overwrite them in C): tp[0] = 0 on unit operands
+        const uint32_t x30p = (uint32_t)(SLOT_OFF_X + 8 * 30);
+        for (int k2 = 0; k2 < HX_SLOT_CAP; k2++) T->hx[k2 * 32 + r] = (uint32_t)SLOT_OFF_TP | x30p << 16 | x30p << 24;
         int n = 0;
         if (r < NV)
             for (int j = 0; j < HT_TERMS; j++)
-                if (U[HX_SIZE + j * HT_PARTS * NV + r] != 0) n++;
+                if (D[j * HT_PARTS * NV + r] != 0) n++;
         s_htn[r] = n;
     }
     __syncthreads();
     if (tid == 0) {
-        int used[HX_NSLOT], order[HX_NSLOT], ne[NV];
+        int used[HX_NSLOT], order[HX_NSLOT];
         for (int s2 = 0; s2 < HX_NSLOT; s2++) { used[s2] = 0; order[s2] = s2; }
         for (int i = 1; i < HX_NSLOT; i++)   // slot classes by capacity, smallest first (stable)
             for (int j2 = i; j2 > 0 && cap[order[j2 - 1]] > cap[order[j2]]; j2--) {
                 const int t2 = order[j2]; order[j2] = order[j2 - 1]; order[j2 - 1] = t2;
             }
-        for (int q = 0; q < 32; q++) {
-            for (int w2 = 0; w2 < 3; w2++) {
-                uint32_t m6 = 0;
-                for (int c = 0; c < 10; c++) m6 |= 6u << (3 * c);
-                s_map[w2][q] = m6;
-            }
+        for (int q = 0; q < 32; q++)
             for (int w2 = 0; w2 < HX_NSLOT / 2; w2++)
                 s_dst[w2][q] = (uint32_t)SLOT_OFF_HXDUMMY | ((uint32_t)SLOT_OFF_HXDUMMY << 16);
-        }
+        int ne[NV], nent = 0;
         for (int q = 0; q < NV; q++) ne[q] = 0;
         for (int n = HX_TERMS; n >= 1; n--)
             for (int row = 0; row < NV; row++)
@@ -479,19 +488,74 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                     int sl = -1;
                     for (int i = 0; i < HX_NSLOT && sl < 0; i++)
                         if (cap[order[i]] >= n && used[order[i]] < 32) sl = order[i];
-                    if (sl < 0 || ne[row] >= 6) { s_bad = 1; continue; }
-                    const int ln = used[sl]++, e = ne[row]++;
+                    if (sl < 0 || ne[row] >= 6 || nent >= ENT_CAP - 1) { s_bad = 1; continue; }
+                    const int ln = used[sl]++;
+                    ne[row]++;
                     s_place[row][c] = (uint8_t)(ln << 3 | sl);
-                    s_map[c / 10][row] = (s_map[c / 10][row] & ~(7u << (3 * (c % 10)))) | ((uint32_t)e << (3 * (c % 10)));
-                    const uint32_t off = (uint32_t)(SLOT_OFF_ENT + (row * 7 + e) * 8);
+                    const uint32_t off = (uint32_t)(SLOT_OFF_ENT + 8 * nent++);
+                    s_eoff[row][c] = (uint16_t)off;
                     const int hi = (sl & 1) * 16;
                     s_dst[sl >> 1][ln] = (s_dst[sl >> 1][ln] & ~(0xFFFFu << hi)) | (off << hi);
                 }
+        // distinct prefixes; a term outside the index ranges is rejected in C
+        int nt = 1, np = 1;
+        s_tri[0] = 33u << 8 | 33u << 16;   // (0, 33, 33): the padding terms' zero prefix
+        s_pair[0] = 33u | 33u << 8;
+        auto add_tri = [&](int co, int a, int b) {
+            const uint32_t key = ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16;
+            for (int i = 0; i < nt; i++) if (s_tri[i] == key) return;
+            if (nt < TP_CAP) s_tri[nt++] = key; else s_bad = 1;
+        };
+        auto add_pair = [&](int a, int b) {
+            const uint32_t key = (uint32_t)a | (uint32_t)b << 8;
+            for (int i = 0; i < np; i++) if (s_pair[i] == key) return;
+            if (np < QP_CAP) s_pair[np++] = key; else s_bad = 1;
+        };
+        for (int i = 0; i < HX_SIZE / HX_PARTS; i++) {   // (column, term, row) triples of dH/dx
+            const int rr = i % NV, cj = i / NV;
+            const int base = cj * HX_PARTS * NV + rr;
+            const int co = U[base], a = U[base + NV], b = U[base + 2 * NV];
+            if (co != 0 && co >= -128 && co <= 127 && a >= 0 && a < NPP && b >= 0 && b < NPP) add_tri(co, a, b);
+        }
+        for (int i = 0; i < HT_SIZE / HT_PARTS; i++) {
+            const int rr = i % NV, j = i / NV;
+            const int base = j * HT_PARTS * NV + rr;
+            const int co = D[base], a = D[base + NV], b = D[base + 2 * NV];
+            if (co != 0 && co >= -128 && co <= 127 && a >= 0 && a < NPP && b >= 0 && b < NPP) {
+                add_tri(co, a, b);
+                add_pair(a, b);
+            }
+        }
+        s_ntri = nt;
+        s_npair = np;
     }
     __syncthreads();
+    auto tp_off = [&](int co, int a, int b) -> uint32_t {
+        const uint32_t key = ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16;
+        for (int i = 0; i < s_ntri; i++) if (s_tri[i] == key) return (uint32_t)(SLOT_OFF_TP + 8 * i);
+        return (uint32_t)SLOT_OFF_TP;
+    };
+    auto qp_off = [&](int a, int b) -> uint32_t {
+        const uint32_t key = (uint32_t)a | (uint32_t)b << 8;
+        for (int i = 0; i < s_npair; i++) if (s_pair[i] == key) return (uint32_t)(SLOT_OFF_QP + 8 * i);
+        return (uint32_t)SLOT_OFF_QP;
+    };
+    const uint32_t x30 = (uint32_t)(SLOT_OFF_X + 8 * 30);
     if (r < 32) {
         bool bad = false;
-        for (int q = 0; q < 3; q++) T->map[q][r] = s_map[q][r];
+        // gather map and structural pattern of row r (padding lanes: zeros)
+        uint32_t pat = 0;
+        for (int q = 0; q < GM_WORDS; q++) {
+            uint32_t v = 0;
+            for (int k2 = 0; k2 < 2; k2++) {
+                const int c = 2 * q + k2;
+                const uint32_t off = r < NV ? s_eoff[r][c] : (uint32_t)SLOT_OFF_ENTZERO;
+                v |= off << (16 * k2);
+                if (off != (uint32_t)SLOT_OFF_ENTZERO) pat |= 1u << c;
+            }
+            T->gm[q][r] = v;
+        }
+        T->pat[r] = pat;
         for (int q = 0; q < HX_NSLOT / 2; q++) T->hxd[q][r] = s_dst[q][r];
         if (r < NV)
             for (int c = 0; c < NV; c++) {
@@ -506,10 +570,8 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                     bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
                            v < 0 || v > NV;
                     if (!bad)
-                        T->hx[pos * 32 + ln] = make_uint2(
-                            (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
-                            (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
-                                (((uint32_t)co & 0xFFu) << 16));
+                        T->hx[pos * 32 + ln] = tp_off(co, a, b) | (uint32_t)(SLOT_OFF_X + 8 * u) << 16 |
+                                               (uint32_t)(SLOT_OFF_X + 8 * v) << 24;
                     pos++;
                 }
             }
@@ -518,13 +580,13 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         // of more than 13 terms (an owner) puts its terms 14.. in its light
         // words 13.. (for x[w]) and in its helper's (lane ^ 16) words 10..; the
         // helper's own terms must end before 10 and it needs no help itself
-        const int32_t *D = U + HX_SIZE;
         const int n = s_htn[r];
         const int need_o = max(0, n - HT_FULL);
         const int need_h = max(0, s_htn[r ^ 16] - HT_FULL);
         if (need_o > 0 && s_htn[r ^ 16] > HT_HELP_FIRST) bad = true;
         if (need_h > 0 && n > HT_HELP_FIRST) bad = true;
-        const uint2 pad_ht = make_uint2(pad_hx.x, pad_hx.y | ((uint32_t)(SLOT_OFF_X + 8 * 30) << 16));
+        const uint2 pad_ht = make_uint2((uint32_t)SLOT_OFF_TP | (uint32_t)SLOT_OFF_QP << 16,
+                                        x30 | x30 << 8 | x30 << 16);   // tp[0], qp[0] with coef 0
         int k = 0;
         if (r < NV) {
             for (int j = 0; j < HT_TERMS; j++) {
@@ -534,11 +596,11 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                 if (co == 0) continue;
                 bad |= co < -128 || co > 127 || a < 0 || a >= NPP || b < 0 || b >= NPP || u < 0 || u > NV ||
                        v < 0 || v > NV || x3 < 0 || x3 > NV;
-                const uint2 tw = make_uint2(
-                    (uint32_t)(SLOT_OFF_P + 8 * a) | ((uint32_t)(SLOT_OFF_P + 8 * b) << 16),
-                    (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
-                        ((uint32_t)(SLOT_OFF_X + 8 * x3) << 16) | (((uint32_t)co & 0xFFu) << 24));
                 if (!bad) {
+                    const uint2 tw = make_uint2(tp_off(co, a, b) | qp_off(a, b) << 16,
+                                                (uint32_t)(SLOT_OFF_X + 8 * u) | ((uint32_t)(SLOT_OFF_X + 8 * v) << 8) |
+                                                    ((uint32_t)(SLOT_OFF_X + 8 * x3) << 16) |
+                                                    (((uint32_t)co & 0xFFu) << 24));
                     T->ht[k * 32 + r] = tw;   // k < 13: a full term; k >= 13: the light word (x[w])
                     if (k >= HT_FULL) T->ht[(HT_HELP_FIRST + k - HT_FULL) * 32 + (r ^ 16)] = tw;
                 }
@@ -547,6 +609,24 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         }
         for (int q = k; q < HT_TERMS; q++)
             if (!(q >= HT_HELP_FIRST && q < HT_HELP_FIRST + need_h)) T->ht[q * 32 + r] = pad_ht;
+        // prefix build jobs of lane r (hc_eval.hpp build_prefixes)
+        const uint32_t p33 = (uint32_t)(SLOT_OFF_STG + 8 * 33);
+        for (int q = 0; q < PRE_ROUNDS; q++) {
+            const bool tpr = q < PRE_TP_ROUNDS;
+            const int i = (tpr ? q : q - PRE_TP_ROUNDS) * 32 + r;
+            uint2 job = make_uint2(p33 | p33 << 16, (uint32_t)SLOT_OFF_HXDUMMY);
+            if (tpr && i < s_ntri) {
+                const uint32_t key = s_tri[i];
+                const uint32_t a = (key >> 8) & 0xFFu, b = key >> 16;
+                job = make_uint2((uint32_t)(SLOT_OFF_STG + 8 * a) | (uint32_t)(SLOT_OFF_STG + 8 * b) << 16,
+                                 (uint32_t)(SLOT_OFF_TP + 8 * i) | (key & 0xFFu) << 16);
+            } else if (!tpr && i < s_npair) {
+                const uint32_t a = s_pair[i] & 0xFFu, b = s_pair[i] >> 8;
+                job = make_uint2((uint32_t)(SLOT_OFF_STG + 8 * a) | (uint32_t)(SLOT_OFF_STG + 8 * b) << 16,
+                                 (uint32_t)(SLOT_OFF_QP + 8 * i));
+            }
+            T->pre[q][r] = job;
+        }
         if (bad) atomicOr(&s_bad, 1);
     }
     __syncthreads();
@@ -648,7 +728,8 @@ typedef uint32_t T_hxd_t[HX_NSLOT / 2][32];
 template <bool ABORT, int MINW, bool GTAB, bool ARCH = false>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     constexpr int LUCH = ABORT ? 4 : LU_CHUNK;   // LU column group (hc_lu.hpp): latency (abort) vs throughput
-    constexpr int TAB_BYTES = GTAB ? 16 : (int)(sizeof(uint2) * (HX_SLOT_CAP + HT_TERMS) * 32 + sizeof(T_hxd_t));
+    constexpr int TAB_BYTES =
+        GTAB ? 16 : (int)(sizeof(uint2) * HT_TERMS * 32 + sizeof(uint32_t) * HX_SLOT_CAP * 32 + sizeof(T_hxd_t));
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
     __shared__ cf s_sp[NPP];
     __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
@@ -657,12 +738,12 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     if (ws->status != 0u) return;
     // time slicing: this launch's ring epoch (bumped by k_prep_tables)
     const unsigned epoch = (!ABORT && a.slice_q > 0) ? ld_rlx(&a.rq[RQ_EPOCH]) : 0u;
-    const uint2 *s_hx = GTAB ? T->hx : reinterpret_cast<const uint2 *>(s_tab);
-    const uint2 *s_ht = GTAB ? T->ht : reinterpret_cast<const uint2 *>(s_tab) + HX_SLOT_CAP * 32;
-    const uint32_t *s_hxd = GTAB ? &T->hxd[0][0] : reinterpret_cast<const uint32_t *>(s_ht + HT_TERMS * 32);
+    const uint2 *s_ht = GTAB ? T->ht : reinterpret_cast<const uint2 *>(s_tab);
+    const uint32_t *s_hx = GTAB ? T->hx : reinterpret_cast<const uint32_t *>(s_ht + HT_TERMS * 32);
+    const uint32_t *s_hxd = GTAB ? &T->hxd[0][0] : s_hx + HX_SLOT_CAP * 32;
     if constexpr (!GTAB) {
-        uint2 *t_hx = reinterpret_cast<uint2 *>(s_tab), *t_ht = t_hx + HX_SLOT_CAP * 32;
-        uint32_t *t_hxd = reinterpret_cast<uint32_t *>(t_ht + HT_TERMS * 32);
+        uint2 *t_ht = reinterpret_cast<uint2 *>(s_tab);
+        uint32_t *t_hx = reinterpret_cast<uint32_t *>(t_ht + HT_TERMS * 32), *t_hxd = t_hx + HX_SLOT_CAP * 32;
         for (int i = threadIdx.x; i < HX_SLOT_CAP * 32; i += WG_THREADS) t_hx[i] = T->hx[i];   // padded table
         for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) t_ht[i] = T->ht[i];
         for (int i = threadIdx.x; i < HX_NSLOT / 2 * 32; i += WG_THREADS) t_hxd[i] = (&T->hxd[0][0])[i];
@@ -679,14 +760,13 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     const int wid = threadIdx.x / WAVE;
     SlotLDS &S = s_slot[wid * 2 + (hb >> 5)];
     if (r == 30) S.x[30] = cmk(1.0f, 0.0f);
-    if (r == 0) S.p[33] = cmk(1.0f, 0.0f);
-    // per-row constants (column->slot maps, structural pattern) live in LDS and
-    // are re-read every stage: held in VGPRs across the loop they spill (abort mode)
+    if (r == 0) S.st.pre_smp = -2;   // no prefix tables yet
+    // per-row constants (gather map, structural pattern) live in LDS and are
+    // re-read every stage: held in VGPRs across the loop they spill (abort mode)
     __shared__ uint32_t s_rowc[GM_WORDS + 1][32];   // [0..14] gather map (hc_eval.hpp), [15] structural pattern
     if (threadIdx.x < 32) {
-        const uint32_t m0[3] = {T->map[0][threadIdx.x], T->map[1][threadIdx.x], T->map[2][threadIdx.x]};
-        for (int q = 0; q < GM_WORDS; q++) s_rowc[q][threadIdx.x] = gather_map_word(m0, threadIdx.x, q);
-        s_rowc[GM_WORDS][threadIdx.x] = row_pattern(m0);   // structural pattern of row r
+        for (int q = 0; q < GM_WORDS; q++) s_rowc[q][threadIdx.x] = T->gm[q][threadIdx.x];
+        s_rowc[GM_WORDS][threadIdx.x] = T->pat[threadIdx.x];
     }
     __syncthreads();
     const bool rl = r < NV;
@@ -716,6 +796,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 #endif
     for (;;) {
         HC_DIAG_MARK(6);
+        HC_ISA_MARK("ctl_slots");
         // ---------------- resolve slot phases until every slot is at a stage or idle
         // next dequeue (time slicing): -1 normal, -2 swap with a suspended path,
         // >= 0 a new-path ticket the suspension claimed (set and used within this phase)
@@ -781,16 +862,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     // suspend block (x in words 0..29, the scalars in 30, 31)
                     b = rb;
                     qpos = 0;
-                    const int smp = b / NTRK;
-                    if (smp != smp_loaded && r < NPP) {
-                        S.tgt[r] = a.target_params[(size_t)smp * NPP + r];
-                        S.dif[r] = a.diff_params[(size_t)smp * NPP + r];
-                    }
-                    if (smp != smp_loaded && r < NPP - 32) {
-                        S.tgt[r + 32] = a.target_params[(size_t)smp * NPP + r + 32];
-                        S.dif[r + 32] = a.diff_params[(size_t)smp * NPP + r + 32];
-                    }
-                    smp_loaded = smp;
+                    smp_loaded = b / NTRK;   // (its target / diff params are read where the prefixes are built)
                     const unsigned long long *blk = a.susp + (size_t)b * SUSP_WORDS;
                     x = rl ? ld_cf_rlx(reinterpret_cast<const cf *>(blk + r)) : cmk(0.0f, 0.0f);
                     xl = x;
@@ -831,16 +903,8 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                         }
                     }
                     if (!skip) {
-                        const int trk = b % NTRK, smp = b / NTRK;            // :67-69
-                        if (smp != smp_loaded && r < NPP) {
-                            S.tgt[r] = a.target_params[(size_t)smp * NPP + r];
-                            S.dif[r] = a.diff_params[(size_t)smp * NPP + r];
-                        }
-                        if (smp != smp_loaded && r < NPP - 32) {
-                            S.tgt[r + 32] = a.target_params[(size_t)smp * NPP + r + 32];
-                            S.dif[r + 32] = a.diff_params[(size_t)smp * NPP + r + 32];
-                        }
-                        smp_loaded = smp;
+                        const int trk = b % NTRK;                            // :67-69
+                        smp_loaded = b / NTRK;
 #ifdef HC_DIAG_TIMES
                         diag_t0 = (int)__builtin_amdgcn_s_memrealtime();
 #endif
@@ -1004,6 +1068,14 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 
         // ---------------- one stage for both slots
         // park the slot state in LDS so it does not occupy VGPRs across eval + LU
+        HC_ISA_MARK("ctl_park");
+        // the slot's prefix tables follow its p(t): rebuilt when t or the
+        // sample changed (about 0.4 times per stage and path; both halves of
+        // the wave rebuild when either needs it, each from its own t and sample)
+        const float pre_t = S.st.pre_t;
+        const int pre_smp = S.st.pre_smp;
+        const bool rebuild = __ballot(ph == PH_STAGE && (__float_as_uint(t0) != __float_as_uint(pre_t) ||
+                                                         smp_loaded != pre_smp)) != 0ull;
         if (r == 0) {
             SlotState q;
             q.t0 = t0; q.t_step = t_step; q.dt = dt; q.h2 = h2; q.scale = scale;
@@ -1011,18 +1083,19 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             q.b = b; q.smp = smp_loaded; q.ph = ph;
             q.flags = (end_zone ? 1 : 0) | (check ? 2 : 0) | (isSucc ? 4 : 0) | (isInf ? 8 : 0) | (piece << 4);
             q.pad = qpos;
+            q.pre_t = rebuild ? t0 : pre_t;
+            q.pre_smp = rebuild ? smp_loaded : pre_smp;
             S.st = q;
         }
         if (rl) { S.x[r] = x; S.xl[r] = xl; S.sols[r] = sols; }
-        {
-            const bool act0 = ph == PH_STAGE;
-            const bool pred0 = act0 && s < 4;
-            if (pred0 && r < NPP - 1) {                                      // :181 p(t), i < 33
-                const float omt = (float)(1.0 - (double)t0);
-                const int rs = lane_fresh() & 31;   // == r; the LDS address is not hoisted and held across the loop
-                S.p[r] = cadd(cscale(S.tgt[r], t0), cscale(s_sp[rs], omt));
-            }
-            if (pred0 && r == 0) S.p[32] = cadd(cscale(S.tgt[32], t0), cscale(s_sp[32], (float)(1.0 - (double)t0)));
+        if (rebuild) {
+            HC_ISA_MARK("ctl_prefix");
+#ifdef HC_DIAG_LUWORK
+            if (lane_fresh() == 0) atomicAdd(&g_diag_luwork[9], 1ull);
+#endif
+            const int rs = lane_fresh() & 31;   // == r; the LDS addresses are not hoisted and held across the loop
+            const size_t so = (size_t)(smp_loaded > 0 ? smp_loaded : 0) * NPP;
+            build_prefixes(S, rs, &T->pre[0][0], a.target_params + so, a.diff_params + so, s_sp, t0);
         }
         wave_lds_sync();
         const int s_in = s, ph_in = ph;
@@ -1039,21 +1112,29 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         // Jacobian registers, so their LDS gathers can run many terms ahead),
         // then dH/dx into rA
         cf rB = cmk(0.0f, 0.0f);
+        HC_ISA_MARK("ev_rhs");
         {
             const bool any_p = __ballot(pred) != 0ull, any_c = __ballot(act && !pred) != 0ull;
             const RhsMasks mk = rhs_masks(T);
+#ifdef HC_DIAG_LUWORK
+            if (lane_v == 0) atomicAdd(&g_diag_luwork[any_p && any_c ? 6 : any_p ? 7 : 8], 1ull);
+#endif
             if (any_p && any_c) {                                            // :185 | :221, one pass
+                HC_ISA_MARK("ev_rhs_mixed");
                 rB = eval_rhs<RHS_MIXED>(s_ht, S, r_v, pred, mk);
             } else if (any_p) {                                              // :185
+                HC_ISA_MARK("ev_rhs_ht");
                 const cf t = eval_rhs<RHS_HT>(s_ht, S, r_v, true, mk);
                 if (pred) rB = t;
             } else if (any_c) {                                              // :221
+                HC_ISA_MARK("ev_rhs_h");
                 const cf t = eval_rhs<RHS_H>(s_ht, S, r_v, false, mk);
                 if (!pred) rB = t;
             }
         }
         HC_DIAG_MARK(3);
         cf rA[NV];
+        HC_ISA_MARK("ev_hx");
         eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_v);                     // :184 / :220
         wave_lds_sync();
         HC_DIAG_MARK(2);
@@ -1064,6 +1145,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 #else
         cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, redo);                  // :188 / :224
 #endif
+        HC_ISA_MARK("ctl_redo");
         if (__builtin_expect(redo, 0)) {
             // a system the sparse solve cannot take exactly (an entry not provably
             // finite, a pivot outside the fast reciprocal range): the Jacobian is
@@ -1071,6 +1153,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             // the right-hand side re-evaluated, and the system solved densely
             // (the stage kind re-read from the parked slot state: held across the
             // LU, act / pred would be spilled)
+            HC_ISA_MARK("redo_evals");
             const bool act_r = S.st.ph == PH_STAGE, pred_r = act_r && S.st.s < 4;
             cf rb = cmk(0.0f, 0.0f);
             if (__ballot(pred_r) != 0ull) {
@@ -1090,6 +1173,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         }
         wave_lds_sync();
         HC_DIAG_MARK(5);
+        HC_ISA_MARK("ctl_update");
         {
             const SlotState q = S.st;
             t0 = q.t0; t_step = q.t_step; dt = q.dt; h2 = q.h2; scale = q.scale;
@@ -1218,7 +1302,7 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restric
 __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws, const cf *__restrict__ X,
                                                      const cf *__restrict__ P, const cf *__restrict__ D,
                                                      cf *__restrict__ HX, cf *__restrict__ HT, cf *__restrict__ H) {
-    __shared__ uint2 s_hx[HX_SLOT_CAP * 32];
+    __shared__ uint32_t s_hx[HX_SLOT_CAP * 32];
     __shared__ uint2 s_ht[HT_TERMS * 32];
     __shared__ uint32_t s_hxd[HX_NSLOT / 2 * 32];
     __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
@@ -1238,18 +1322,19 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
     SlotLDS &S = s_slot[(threadIdx.x / WAVE) * 2 + (lane >> 5)];
     const bool ok = sys < n;
     if (ok && r < 31) S.x[r] = X[(size_t)sys * 31 + r];
-    if (ok) {
-        S.p[r] = P[(size_t)sys * NPP + r];
-        S.dif[r] = D[(size_t)sys * NPP + r];
-        if (r < NPP - 32) { S.p[r + 32] = P[(size_t)sys * NPP + r + 32]; S.dif[r + 32] = D[(size_t)sys * NPP + r + 32]; }
+    if (ok) {   // the point's p and d, staged for the prefix tables
+        S.ent[r] = P[(size_t)sys * NPP + r];
+        S.ent[NPP + r] = D[(size_t)sys * NPP + r];
+        if (r < NPP - 32) {
+            S.ent[r + 32] = P[(size_t)sys * NPP + r + 32];
+            S.ent[NPP + r + 32] = D[(size_t)sys * NPP + r + 32];
+        }
     }
     __shared__ uint32_t s_gm[GM_WORDS][32];
-    if (threadIdx.x < 32) {
-        const uint32_t m0[3] = {T->map[0][threadIdx.x], T->map[1][threadIdx.x], T->map[2][threadIdx.x]};
-        for (int q = 0; q < GM_WORDS; q++) s_gm[q][threadIdx.x] = gather_map_word(m0, threadIdx.x, q);
-    }
+    if (threadIdx.x < 32)
+        for (int q = 0; q < GM_WORDS; q++) s_gm[q][threadIdx.x] = T->gm[q][threadIdx.x];
     __syncthreads();
-    wave_lds_sync();
+    build_prefix_rounds(S, r, &T->pre[0][0]);
     cf rA[NV];
     eval_hx(rA, s_hx, s_hxd, &s_gm[0][0], S, r);
     const cf ht = eval_rhs<RHS_HT>(s_ht, S, r, true, rhs_masks(T));
@@ -1419,9 +1504,11 @@ int hc_diag_phases(unsigned long long *out, int reset) {
 
 #ifdef HC_DIAG_LUWORK
 int hc_diag_luwork(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_luwork), sizeof(unsigned long long) * 3) != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_luwork), sizeof(unsigned long long) * hc::DIAG_LUWORK_WORDS) !=
+        hipSuccess)
+        return -1;
     if (reset) {
-        static const unsigned long long z[3] = {0, 0, 0};
+        static const unsigned long long z[hc::DIAG_LUWORK_WORDS] = {0};
         if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_luwork), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;

@@ -113,15 +113,6 @@ __device__ __forceinline__ int half_min_int_p16(int v) {
     return min((int)sw[0], (int)sw[1]);
 }
 
-// structural pattern of row r from its column->entry-slot map (slot 6 = zero)
-__device__ __forceinline__ uint32_t row_pattern(const uint32_t (&map)[3]) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int c = 0; c < NV; c++)
-        if (((map[c / 10] >> (3 * (c % 10))) & 7u) != 6u) m |= 1u << c;
-    return m;
-}
-
 // reciprocals (o1, o2) of the cuCdivf factors of the pivot a lane owns, kept
 // from the forward step that chose it (brs, bis = pivot * o1 are recomputed
 // from the pivot element, which stays in the owner's rA)
@@ -209,8 +200,13 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uin
 #ifdef HC_DIAG_LUWORK
 // diagnostic build: rank-1 update elements the solves execute (sum over the
 // executed column groups of columns x active lanes), and the solves
-__device__ unsigned long long g_diag_luwork[3];   // executed elements and completed sparse solves; dense solves
-struct LuWork { unsigned long long acc, mask; };   // mask: lanes whose work counts (active path slots)
+// [0] executed elements, [1] completed sparse solves, [2] dense solves (path
+// solves); wave-level: [3] sparse wave-solves, [4] live column groups, [5] rare
+// pivot steps; [6..8] stages whose right-hand side ran the mixed / dH/dt-only /
+// H-only evaluation, [9] stages that rebuilt the prefix tables (k_track)
+constexpr int DIAG_LUWORK_WORDS = 10;
+__device__ unsigned long long g_diag_luwork[DIAG_LUWORK_WORDS];
+struct LuWork { unsigned long long acc, mask, groups, rare; };   // mask: lanes whose work counts (active path slots)
 #define HC_LU_WORK(ncols) (lu_work_acc.acc += (unsigned long long)(ncols) * \
     (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask))
 #define HC_LU_WORK_ARG , LuWork &lu_work_acc
@@ -231,6 +227,9 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
         constexpr int J = C::start(I, K), N = C::len(I, K);
         if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
             HC_LU_WORK(N);
+#ifdef HC_DIAG_LUWORK
+            lu_work_acc.groups++;
+#endif
             cf u[N];
             if constexpr (N == 1) {
                 u[0] = L.row[J];
@@ -266,6 +265,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         pmw = (pp0 | pp1) & FULL;
     }
     const uint32_t gb = group_bits<CH>(pmw);
+    HC_ISA_MARK_I("lu_store", I);
     if (is_piv) {                                          // pivot row -> buffer
         L.row[I] = rA[I];
         lu_put_row<I, 0, CH>(rA, pmw, gb, L);
@@ -273,6 +273,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         L.row[31].x = __int_as_float(rowid);
     }
     wave_lds_sync();
+    HC_ISA_MARK_I("lu_rcp", I);
     const cf sxi = L.row[I];
     cf sB0, pr;
     ld4(&L.row[30], sB0, pr);
@@ -302,11 +303,13 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // below whose column I may be non-zero takes the pivot patterns (both
     // halves': a superset of its own pivot row's).
     if (below) {
+        HC_ISA_MARK_I("lu_mult", I);
         const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
         const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
         rB = cmk(bp.x, bp.y);
         // v_bfe_i32 + v_and_or_b32
         if constexpr (!DENSE) pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
+        HC_ISA_MARK_I("lu_update", I);
         lu_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
     }
 }
@@ -318,6 +321,7 @@ template <int I, bool DENSE, int CH>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
                                            bool row_lane, PivF &my, LUBuf &L, bool &redo HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
+        HC_ISA_MARK_I("lu_search", I);
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
         const bool elig = rowid >= I && row_lane;
         bool is_piv;
@@ -332,6 +336,10 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         // per-half m & (m - 1) tests took six SALU), both in the fast range
         const bool rare = DENSE || (__builtin_popcountll(m) != 2) | (bad != 0ull);
         if (__builtin_expect(rare, 0)) {
+            HC_ISA_MARK_I("lu_rare", I);
+#ifdef HC_DIAG_LUWORK
+            lu_work_acc.rare++;
+#endif
             // rare: NaN at position I wins (:57-64); exact ties: first position wins
             const bool isn = v != v;
             const unsigned long long nanb = __builtin_amdgcn_ballot_w64(isn);
@@ -366,6 +374,7 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl0 = __builtin_ctz(mlo);        // exactly one bit per half here
             pl1 = 32 + __builtin_ctz(mhi);
         }
+        HC_ISA_MARK_I("lu_pattern", I);
         lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
         lu_forward<I + 1, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo HC_LU_WORK_PASS);
     }
@@ -382,6 +391,7 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
 template <int I>
 __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowid, const PivF &my, pf2 &res) {
     if constexpr (I >= 0) {
+        HC_ISA_MARK_I("lu_back", I);
         const unsigned long long own = __builtin_amdgcn_ballot_w64(rowid == I);
         const int o0 = __builtin_ctz((unsigned)own);          // one owner per half
         const int o1 = 32 + __builtin_ctz((unsigned)(own >> 32));
@@ -425,6 +435,9 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     const int r = lane & 31, hb = lane & 32;
     const bool row_lane = r < NV;
     redo = false;
+    if constexpr (DENSE) HC_ISA_MARK("lu_dense");   // (scripts/isa_phases.py: the dense re-solve's copy)
+    else HC_ISA_MARK("lu_sparse");
+    HC_ISA_MARK("lu_finite");
     if constexpr (!DENSE) {
         // every entry finite and below 2^64 in magnitude (inside the 2^88 the
         // sparse path needs): the per-component sums of squares (v_pk_fma_f32, 30
@@ -447,18 +460,22 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     uint32_t pat = row_lane ? pattern : 0u;
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
-    LuWork lu_work_acc{0ull, count_mask};
+    LuWork lu_work_acc{0ull, count_mask, 0ull, 0ull};
     lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
     if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
         atomicAdd(&g_diag_luwork[1], solves);
+        atomicAdd(&g_diag_luwork[3], 1ull);
+        atomicAdd(&g_diag_luwork[4], lu_work_acc.groups);
+        atomicAdd(&g_diag_luwork[5], lu_work_acc.rare);
     }
     if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
     lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
+    HC_ISA_MARK("lu_back_init");
     pf2 res = {0.0f, 0.0f};
     lu_backward<NV - 1>(rA, rB, rowid, my, res);
     return cmk(res.x, res.y);

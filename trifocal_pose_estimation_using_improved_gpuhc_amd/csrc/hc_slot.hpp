@@ -19,21 +19,33 @@ struct SlotState {
     float t0, t_step, dt, h2, scale;
     int s, stepidx, coef, succ, nsteps, ncorr, b, smp, ph, flags;
     int pad;
+    // the (t, sample) the slot's prefix tables were built for (hc_eval.hpp
+    // build_prefixes): they are rebuilt only when p(t) changes
+    float pre_t;
+    int pre_smp;
 };
+// Capacities of the per-slot prefix tables (hc_eval.hpp): the distinct
+// (coef, a, b) triples of the dH/dx and H terms (93 in this problem,
+// padding term included) and the distinct (a, b) pairs of the dH/dt terms (38).
+constexpr int TP_CAP = 96, QP_CAP = 40;
+// dH/dx entries in the slot (hc_kernels.hip k_prep_tables packs them; the
+// problem has 170): ENT_CAP - 1 is the structural zero, written once per launch.
+constexpr int ENT_CAP = 172;
 // per path-slot LDS block
 struct alignas(16) SlotLDS {
     cf x[32];        // current track (x[30] = 1)
     cf xl[32];       // last successful track
     cf sols[32];     // RK accumulator
-    cf p[NPP];       // p(t)
-    cf tgt[NPP];     // target params
-    cf dif[NPP];     // diff params
-    cf ent[NV * 7];  // dH/dx entries of row r at [r*7 + slot], slot 6 = 0 (kept through the LU)
+    cf ent[ENT_CAP]; // dH/dx entries, packed (k_prep_tables; kept through the LU); p(t) and the
+                     // diff params are staged in its first 68 entries while the prefixes are built
     cf lu[32];       // the LU's pivot-row buffer (hc_lu.hpp LUBuf)
+    cf tp[TP_CAP];   // prefix table T: (c * p[a]) * p[b] per (c, a, b) triple (dH/dx and H terms)
+    cf qp[QP_CAP];   // prefix table Q: d[a] * p[b] + d[b] * p[a] per (a, b) pair (dH/dt terms)
     SlotState st;
-    char bank_pad[16];   // slot stride = 16 mod 256 B: the slots of one wave (same offsets,
+    char bank_pad[40];   // slot stride = 16 mod 256 B: the slots of one wave (same offsets,
                          // different bases) land on different LDS banks
 };
 static_assert(sizeof(SlotLDS) % 256 == 16, "SlotLDS stride must shift the LDS banks by 4 per slot");
+static_assert(sizeof(SlotLDS) <= 3600, "5 workgroups per CU: 8 slots + the workgroup's tables in 32 KB");
 
 }  // namespace hc
