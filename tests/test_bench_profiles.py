@@ -1,0 +1,46 @@
+"""bench.py's profile selection (CPU): the roofline's traffic and executed-LU
+figures come only from committed profiles stamped with the loaded library's
+build id, newest by the timestamp recorded inside each file (not by name)."""
+import json
+import os
+
+import bench
+
+
+def _write(d, name, payload, jsonl=False):
+    p = os.path.join(d, "profiles", name)
+    with open(p, "w") as fh:
+        if jsonl:
+            fh.write("log line\n" + json.dumps(payload) + "\n")
+        else:
+            json.dump(payload, fh)
+
+
+def test_selection_by_build_id_and_timestamp(tmp_path, monkeypatch):
+    os.makedirs(tmp_path / "profiles")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    k = bench.TRACK_KERNEL
+    # a later-sorting name from another build must not win
+    _write(tmp_path, "r9z_pmc_summary.json",
+           {"build_id": "v0+other", "kernel": k, "measured_at": "2099", "derived": {"hbm_bytes_per_launch": 1}})
+    _write(tmp_path, "r4aa_pmc_summary.json",
+           {"build_id": "v1+abc", "kernel": k, "measured_at": "2026-10-17T10:00", "derived": {"hbm_bytes_per_launch": 7}})
+    _write(tmp_path, "r4b_pmc_summary.json",
+           {"build_id": "v1+abc", "kernel": k, "measured_at": "2026-10-17T09:00", "derived": {"hbm_bytes_per_launch": 5}})
+    _write(tmp_path, "r4c_pmc_summary.json",   # same build, another kernel: skipped
+           {"build_id": "v1+abc", "kernel": "other", "measured_at": "2027", "derived": {"hbm_bytes_per_launch": 3}})
+    v, src = bench.traffic_bytes(k, "v1+abc")
+    assert v == 7 and src == os.path.join("profiles", "r4aa_pmc_summary.json")
+    v, why = bench.traffic_bytes(k, "v1+none")
+    assert v is None and "v1+none" in why
+
+
+def test_lu_fraction_skips_scaled_runs(tmp_path, monkeypatch):
+    os.makedirs(tmp_path / "profiles")
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    _write(tmp_path, "a_lu_work.json", {"build_id": "b", "measured_at": "2", "config": "config 2 scaled x10",
+                                        "executed_fraction": 0.9}, jsonl=True)
+    _write(tmp_path, "b_lu_work.json", {"build_id": "b", "measured_at": "1", "config": "config 2",
+                                        "executed_fraction": 0.42}, jsonl=True)
+    v, src = bench.lu_executed_fraction("b")
+    assert v == 0.42 and src.endswith("b_lu_work.json")
