@@ -2,7 +2,7 @@
 # build (scripts/profile.sh), and the LU-work count of the same sources
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-T=${1:-r4a}
+T=${1:-r4g}
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > gpurun_out/${T}_pytest.log 2>&1; rc=$?; tail -3 gpurun_out/${T}_pytest.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 500 python bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err; rc=$?; cat gpurun_out/${T}_bench.json; [ $rc -eq 0 ] || exit $rc
 bash scripts/profile.sh ${T} || exit 1

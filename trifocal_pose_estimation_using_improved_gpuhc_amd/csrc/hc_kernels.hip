@@ -439,6 +439,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
     __shared__ uint32_t s_tri[TP_CAP];    // (uint8)c | a << 8 | b << 16
     __shared__ uint32_t s_pair[QP_CAP];   // a | b << 8
     __shared__ int s_ntri, s_npair;
+    __shared__ uint32_t s_th[256], s_ph[128];   // hash sets of the prefix keys (+ 1)
     // slot capacities and starts as locals (a runtime index into the
     // namespace-scope constexpr table does not reach device memory)
     int cap[HX_NSLOT], start[HX_NSLOT];
@@ -458,6 +459,41 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
             s_place[r][c] = 0xFFu;
             s_eoff[r][c] = (uint16_t)SLOT_OFF_ENTZERO;
         }
+    // the distinct prefix keys of all terms, collected by every thread into LDS
+    // hash sets (open addressing, atomicCAS; key + 1, 0 = empty); a term outside
+    // the index ranges is left out here and rejected in C
+    for (int h = tid; h < 256; h += PREP_THREADS) s_th[h] = 0u;
+    for (int h = tid; h < 128; h += PREP_THREADS) s_ph[h] = 0u;
+    __syncthreads();
+    {
+        auto hins = [&](uint32_t *tab, uint32_t mask, uint32_t key) {
+            uint32_t h = (key * 2654435761u) >> 20 & mask;
+            for (uint32_t probe = 0; probe <= mask; probe++) {
+                const uint32_t old = atomicCAS(&tab[h], 0u, key + 1u);
+                if (old == 0u || old == key + 1u) return;
+                h = (h + 1u) & mask;
+            }
+            s_bad = 1;   // more distinct keys than the set holds
+        };
+        for (int i = tid; i < HX_SIZE / HX_PARTS; i += PREP_THREADS) {   // (column, term, row) of dH/dx
+            const int base = (i / NV) * HX_PARTS * NV + i % NV;
+            const int co = U[base];
+            if (co == 0) continue;
+            const int a = U[base + NV], b = U[base + 2 * NV];
+            if (co >= -128 && co <= 127 && a >= 0 && a < NPP && b >= 0 && b < NPP)
+                hins(s_th, 255u, ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16);
+        }
+        for (int i = tid; i < HT_SIZE / HT_PARTS; i += PREP_THREADS) {
+            const int base = (i / NV) * HT_PARTS * NV + i % NV;
+            const int co = D[base];
+            if (co == 0) continue;
+            const int a = D[base + NV], b = D[base + 2 * NV];
+            if (co >= -128 && co <= 127 && a >= 0 && a < NPP && b >= 0 && b < NPP) {
+                hins(s_th, 255u, ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16);
+                hins(s_ph, 127u, (uint32_t)a | (uint32_t)b << 8);
+            }
+        }
+    }
     if (r < 32) {
         // padding words first (other lanes' rows overwrite them in C): tp[0] = 0 on unit operands
         const uint32_t x30p = (uint32_t)(SLOT_OFF_X + 8 * 30);
@@ -497,48 +533,50 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
                     const int hi = (sl & 1) * 16;
                     s_dst[sl >> 1][ln] = (s_dst[sl >> 1][ln] & ~(0xFFFFu << hi)) | (off << hi);
                 }
-        // distinct prefixes; a term outside the index ranges is rejected in C
+        // the distinct prefixes, from the hash sets below: (0, 33, 33) and (33, 33)
+        // first (the padding words point at slot 0), the others in key order
         int nt = 1, np = 1;
-        s_tri[0] = 33u << 8 | 33u << 16;   // (0, 33, 33): the padding terms' zero prefix
-        s_pair[0] = 33u | 33u << 8;
-        auto add_tri = [&](int co, int a, int b) {
-            const uint32_t key = ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16;
-            for (int i = 0; i < nt; i++) if (s_tri[i] == key) return;
-            if (nt < TP_CAP) s_tri[nt++] = key; else s_bad = 1;
-        };
-        auto add_pair = [&](int a, int b) {
-            const uint32_t key = (uint32_t)a | (uint32_t)b << 8;
-            for (int i = 0; i < np; i++) if (s_pair[i] == key) return;
-            if (np < QP_CAP) s_pair[np++] = key; else s_bad = 1;
-        };
-        for (int i = 0; i < HX_SIZE / HX_PARTS; i++) {   // (column, term, row) triples of dH/dx
-            const int rr = i % NV, cj = i / NV;
-            const int base = cj * HX_PARTS * NV + rr;
-            const int co = U[base], a = U[base + NV], b = U[base + 2 * NV];
-            if (co != 0 && co >= -128 && co <= 127 && a >= 0 && a < NPP && b >= 0 && b < NPP) add_tri(co, a, b);
+        const uint32_t pad_t = 33u << 8 | 33u << 16, pad_p = 33u | 33u << 8;
+        s_tri[0] = pad_t;
+        s_pair[0] = pad_p;
+        for (int h = 0; h < 256; h++) {
+            const uint32_t k = s_th[h] - 1u;
+            if (s_th[h] == 0u || k == pad_t) continue;
+            if (nt < TP_CAP) s_tri[nt++] = k; else s_bad = 1;
         }
-        for (int i = 0; i < HT_SIZE / HT_PARTS; i++) {
-            const int rr = i % NV, j = i / NV;
-            const int base = j * HT_PARTS * NV + rr;
-            const int co = D[base], a = D[base + NV], b = D[base + 2 * NV];
-            if (co != 0 && co >= -128 && co <= 127 && a >= 0 && a < NPP && b >= 0 && b < NPP) {
-                add_tri(co, a, b);
-                add_pair(a, b);
+        for (int h = 0; h < 128; h++) {
+            const uint32_t k = s_ph[h] - 1u;
+            if (s_ph[h] == 0u || k == pad_p) continue;
+            if (np < QP_CAP) s_pair[np++] = k; else s_bad = 1;
+        }
+        for (int i = 2; i < nt; i++)
+            for (int j2 = i; j2 > 1 && s_tri[j2 - 1] > s_tri[j2]; j2--) {
+                const uint32_t t2 = s_tri[j2]; s_tri[j2] = s_tri[j2 - 1]; s_tri[j2 - 1] = t2;
             }
-        }
+        for (int i = 2; i < np; i++)
+            for (int j2 = i; j2 > 1 && s_pair[j2 - 1] > s_pair[j2]; j2--) {
+                const uint32_t t2 = s_pair[j2]; s_pair[j2] = s_pair[j2 - 1]; s_pair[j2 - 1] = t2;
+            }
         s_ntri = nt;
         s_npair = np;
     }
     __syncthreads();
+    // slot of a key: 0 for the padding key, else binary search in the sorted rest
+    auto find = [](const uint32_t *tab, int n, uint32_t key) -> int {
+        if (key == tab[0]) return 0;
+        int lo = 1, hi = n;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (tab[mid] < key) lo = mid + 1; else hi = mid;
+        }
+        return lo < n && tab[lo] == key ? lo : 0;
+    };
     auto tp_off = [&](int co, int a, int b) -> uint32_t {
-        const uint32_t key = ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16;
-        for (int i = 0; i < s_ntri; i++) if (s_tri[i] == key) return (uint32_t)(SLOT_OFF_TP + 8 * i);
-        return (uint32_t)SLOT_OFF_TP;
+        return (uint32_t)(SLOT_OFF_TP +
+                          8 * find(s_tri, s_ntri, ((uint32_t)co & 0xFFu) | (uint32_t)a << 8 | (uint32_t)b << 16));
     };
     auto qp_off = [&](int a, int b) -> uint32_t {
-        const uint32_t key = (uint32_t)a | (uint32_t)b << 8;
-        for (int i = 0; i < s_npair; i++) if (s_pair[i] == key) return (uint32_t)(SLOT_OFF_QP + 8 * i);
-        return (uint32_t)SLOT_OFF_QP;
+        return (uint32_t)(SLOT_OFF_QP + 8 * find(s_pair, s_npair, (uint32_t)a | (uint32_t)b << 8));
     };
     const uint32_t x30 = (uint32_t)(SLOT_OFF_X + 8 * 30);
     if (r < 32) {
@@ -609,14 +647,91 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         }
         for (int q = k; q < HT_TERMS; q++)
             if (!(q >= HT_HELP_FIRST && q < HT_HELP_FIRST + need_h)) T->ht[q * 32 + r] = pad_ht;
-        // prefix build jobs of lane r (hc_eval.hpp build_prefixes)
+        if (bad) atomicOr(&s_bad, 1);
+    }
+    // E: bank-aware places of the (c, a, b) prefixes.  A ds_read_b64 of tp[]
+    // serves 32 lanes a cycle when their indices differ mod 32 (or coincide);
+    // the words of C read tp at 21 dH/dx and 13 rhs positions, and the sorted
+    // numbering above costs ~64 cycles where 34 are the minimum.  Prefixes that
+    // share a read position (conflict graph, s_adj) go to different residues:
+    // the padding prefix first (tp[0]), then by degree, each to the residue
+    // with the fewest conflicts and a free place (3 per residue, ties: fewer
+    // used, then the lower residue); C's words are renumbered after it.
+    // Places only: the values and their operations stay the same (bit-exact).
+    __shared__ uint32_t s_adj[TP_CAP][3];
+    __shared__ uint8_t s_pidx[HX_SLOT_CAP + HT_FULL][32];
+    __shared__ uint8_t s_tslot[TP_CAP], s_tinv[TP_CAP], s_order[TP_CAP];
+    __shared__ int s_deg[TP_CAP];
+    for (int i = tid; i < TP_CAP * 3; i += PREP_THREADS) (&s_adj[0][0])[i] = 0u;
+    for (int i = tid; i < TP_CAP; i += PREP_THREADS) { s_tinv[i] = 0xFFu; s_tslot[i] = 0u; }
+    __syncthreads();
+    const int ntri = s_ntri;
+    auto tp_index = [&](uint32_t w) -> uint32_t {   // sorted index of a word's tp offset (TP_CAP: none)
+        const uint32_t o = w & 0xFFFFu;
+        const uint32_t i = (o - (uint32_t)SLOT_OFF_TP) / 8u;
+        return o >= (uint32_t)SLOT_OFF_TP && i < (uint32_t)ntri ? i : (uint32_t)TP_CAP;
+    };
+    for (int i = tid; i < (HX_SLOT_CAP + HT_FULL) * 32; i += PREP_THREADS) {
+        const int p = i >> 5, l = i & 31;
+        const uint32_t w = p < HX_SLOT_CAP ? T->hx[p * 32 + l] : T->ht[(p - HX_SLOT_CAP) * 32 + l].x;
+        s_pidx[p][l] = (uint8_t)min(tp_index(w), (uint32_t)0xFFu);
+    }
+    __syncthreads();
+    for (int i = tid; i < (HX_SLOT_CAP + HT_FULL) * 32; i += PREP_THREADS) {
+        const int p = i >> 5, l = i & 31;
+        const uint32_t t = s_pidx[p][l];
+        if (t >= (uint32_t)ntri) continue;
+        for (int l2 = 0; l2 < 32; l2++) {
+            const uint32_t u = s_pidx[p][l2];
+            if (u != t && u < (uint32_t)ntri) atomicOr(&s_adj[t][u >> 5], 1u << (u & 31));
+        }
+    }
+    __syncthreads();
+    if (tid < ntri)
+        s_deg[tid] = tid == 0 ? (1 << 20) : __popc(s_adj[tid][0]) + __popc(s_adj[tid][1]) + __popc(s_adj[tid][2]);
+    __syncthreads();
+    if (tid < ntri) {   // rank by degree, descending (ties: lower index first)
+        int rk = 0;
+        const int d = s_deg[tid];
+        for (int u = 0; u < ntri; u++) rk += (s_deg[u] > d || (s_deg[u] == d && u < tid)) ? 1 : 0;
+        s_order[rk] = (uint8_t)tid;
+    }
+    __syncthreads();
+    if (tid < 64) {   // wave 0, lane c < 32: residue c (its members and fill)
+        uint32_t m0 = 0u, m1 = 0u, m2 = 0u;
+        int fill = 0;
+        for (int k2 = 0; k2 < ntri; k2++) {
+            const int t = s_order[k2];
+            const int conf = __popc(s_adj[t][0] & m0) + __popc(s_adj[t][1] & m1) + __popc(s_adj[t][2] & m2);
+            int key = (tid < 32 && fill < 3) ? ((conf * 4 + fill) << 5 | tid) : 0x7FFFFFFF;
+            for (int s2 = 32; s2 > 0; s2 >>= 1) key = min(key, __shfl_xor(key, s2, 64));
+            if (tid == (key & 31)) {
+                const int slot = tid + 32 * fill++;
+                s_tslot[t] = (uint8_t)slot;
+                s_tinv[slot] = (uint8_t)t;
+                if (t < 32) m0 |= 1u << t; else if (t < 64) m1 |= 1u << (t - 32); else m2 |= 1u << (t - 64);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < HX_SLOT_CAP * 32; i += PREP_THREADS) {
+        const uint32_t w = T->hx[i], t = tp_index(w);
+        if (t < (uint32_t)TP_CAP) T->hx[i] = (w & ~0xFFFFu) | (uint32_t)(SLOT_OFF_TP + 8 * s_tslot[t]);
+    }
+    for (int i = tid; i < HT_TERMS * 32; i += PREP_THREADS) {
+        const uint32_t w = T->ht[i].x, t = tp_index(w);
+        if (t < (uint32_t)TP_CAP) T->ht[i].x = (w & ~0xFFFFu) | (uint32_t)(SLOT_OFF_TP + 8 * s_tslot[t]);
+    }
+    if (r < 32) {
+        // prefix build jobs of lane r (hc_eval.hpp build_prefixes): tp place i
+        // holds prefix s_tinv[i], qp place i pair i
         const uint32_t p33 = (uint32_t)(SLOT_OFF_STG + 8 * 33);
         for (int q = 0; q < PRE_ROUNDS; q++) {
             const bool tpr = q < PRE_TP_ROUNDS;
             const int i = (tpr ? q : q - PRE_TP_ROUNDS) * 32 + r;
             uint2 job = make_uint2(p33 | p33 << 16, (uint32_t)SLOT_OFF_HXDUMMY);
-            if (tpr && i < s_ntri) {
-                const uint32_t key = s_tri[i];
+            if (tpr && i < TP_CAP && s_tinv[i] != 0xFFu) {
+                const uint32_t key = s_tri[s_tinv[i]];
                 const uint32_t a = (key >> 8) & 0xFFu, b = key >> 16;
                 job = make_uint2((uint32_t)(SLOT_OFF_STG + 8 * a) | (uint32_t)(SLOT_OFF_STG + 8 * b) << 16,
                                  (uint32_t)(SLOT_OFF_TP + 8 * i) | (key & 0xFFu) << 16);
@@ -627,7 +742,6 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
             }
             T->pre[q][r] = job;
         }
-        if (bad) atomicOr(&s_bad, 1);
     }
     __syncthreads();
     if (r == 0) {
@@ -1200,7 +1314,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     x = cadd(x, cmul(k, cmk(s == 2 ? dt : h2, 0.0f)));
                     if (s != 1) t0 += h2;
                 } else if (s < 3) {                                          // :191-205
-                    const float w = (float)((double)coef * 1.0 / 6.0);
+                    // (double)coef * 1.0 / 6.0 rounded to float; coef is 1 or 2 here
+                    // (it doubles after s = 0 and s = 2): a constant each, so no f64 division
+                    const float w = coef == 1   ? (float)(1.0 / 6.0)
+                                    : coef == 2 ? (float)(2.0 / 6.0)
+                                                : (float)((double)coef * 1.0 / 6.0);
                     sols = cadd(sols, cscale(cscale(k, dt), w));
                     if (coef > 1) x = xl;
                     const int sc = (s == 1) ? 0 : 1;
@@ -1706,8 +1824,8 @@ int hc_trifocal_abi_version(void) { return HC_TRIFOCAL_ABI_VERSION; }
 void hc_trifocal_set_ring_test(int delay_ticks) { hc::g_ring_test = delay_ticks > 0 ? delay_ticks : 0; }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.4 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
-           "readlane back substitution, pipelined evals with entry-grouped dH/dx terms, 5 waves/SIMD, time slicing "
+    return "hc_trifocal gfx950 v9.5 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
+           "readlane back substitution, pipelined evals over per-slot prefix tables, 5 waves/SIMD, time slicing "
            "at step boundaries with least-attained-service issue priority)";
 }
 

@@ -123,13 +123,17 @@ struct PivF { pf2 oo; };
 // 1/y = ((o1*brs)*o2, (-(o1*bis))*o2); -(o1*bis) is computed as o1*(-bis)
 // (IEEE: the same value).  oo returns (o1, o2).
 __device__ __forceinline__ pf2 recip_fast(pf2 y, float s, pf2 &oo) {
-    oo.x = rcp_rn(s);
-    pf2 bb, sq, q, r;
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(bb) : "v"(y), "v"(oo));
+    // o1 and o2 each in a pair of their own (low half), broadcast by op_sel:
+    // no copy to place them side by side
+    pf2 o1p, o2p, bb, sq, q, r;
+    o1p.x = rcp_rn(s);
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(bb) : "v"(y), "v"(o1p));
     asm("v_pk_mul_f32 %0, %1, %1" : "=v"(sq) : "v"(bb));
-    oo.y = rcp_rn(sq.x + sq.y);
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(q) : "v"(oo), "v"(bb));
-    asm("v_pk_mul_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,1]" : "=v"(r) : "v"(q), "v"(oo));
+    o2p.x = rcp_rn(sq.x + sq.y);
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[0,1] neg_hi:[0,1]" : "=v"(q) : "v"(o1p), "v"(bb));
+    asm("v_pk_mul_f32 %0, %1, %2 op_sel_hi:[1,0]" : "=v"(r) : "v"(q), "v"(o2p));
+    oo.x = o1p.x;
+    oo.y = o2p.x;
     return r;
 }
 
@@ -334,7 +338,12 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
         const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
         // common: one maximum per half (two in the wave; s_bcnt1, where the
         // per-half m & (m - 1) tests took six SALU), both in the fast range
-        const bool rare = DENSE || (__builtin_popcountll(m) != 2) | (bad != 0ull);
+        // the pivot steps where exact ties are frequent on this problem's Jacobians
+        // (steps 18, 19, 21, 22: 79, 29, 51, 32 % of solves) resolve them inline
+        // with one more half-wave min reduction (lowest row id among the maxima)
+        // instead of taking the rare path (profiles/r4f_ab_trims.jsonl)
+        constexpr bool TIE = I == 18 || I == 19 || I == 21 || I == 22;
+        const bool rare = DENSE || (TIE ? (bad != 0ull) : ((__builtin_popcountll(m) != 2) | (bad != 0ull)));
         if (__builtin_expect(rare, 0)) {
             HC_ISA_MARK_I("lu_rare", I);
 #ifdef HC_DIAG_LUWORK
@@ -368,6 +377,15 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl1 = 32 + __builtin_ctz((unsigned)(pm >> 32) | 0x80000000u);
             if constexpr (!DENSE)
                 redo = redo || __builtin_amdgcn_ballot_w64(!rcp_fast_bits(__float_as_int(piv_abs))) != 0ull;
+        } else if constexpr (TIE) {
+            // first position (lowest row id) among each half's maxima
+            const int c2 = key == mx ? rowid : (1 << 20);
+            const int mn = half_min_int_p16(c2);
+            is_piv = key == mx && rowid == mn;
+            piv_abs = __int_as_float(mx);
+            const unsigned long long w = __builtin_amdgcn_ballot_w64(is_piv);
+            pl0 = __builtin_ctz((unsigned)w);
+            pl1 = 32 + __builtin_ctz((unsigned)(w >> 32));
         } else {
             is_piv = key == mx;
             piv_abs = __int_as_float(mx);
