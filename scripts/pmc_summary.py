@@ -79,6 +79,17 @@ try:
     if "SQ_INSTS_VALU" in c:
         ex = rl.get("executed_gflop_per_launch")
         de = rl.get("dense_lu_gflop_per_launch", rl.get("algorithmic_gflop_per_launch"))
+        if not ex and de and rl.get("rk4_steps") is not None:
+            # the bench run predates this build's LU-work profile: the same
+            # pricing as bench.py, from the committed profile of the build
+            sys.path.insert(0, ROOT)
+            import bench
+            frac, src = bench.lu_executed_fraction(out["build_id"])
+            if frac is not None:
+                stages = 4 * rl["rk4_steps"] + rl["corrections"]
+                ex = de - stages * bench.LU_UPDATE_DENSE_FLOP * (1.0 - frac) / 1e9
+                out["lu_executed_fraction"] = frac
+                out["lu_executed_fraction_source"] = src
         if ex:
             der["flop_per_valu_executed"] = ex * 1e9 / c["SQ_INSTS_VALU"]
         if de:
