@@ -20,6 +20,18 @@ stats = list(csv.DictReader(open(os.path.join(base, f"{tag}_trace", "run_kernel_
 trk = [r for r in stats if r["Name"] == KNAME][0]
 out = {"tag": tag, "build_id": None, "measured_at": None, "kernel": trk["Name"], "calls": int(trk["Calls"]), "avg_ns": float(trk["AverageNs"]),
        "min_ns": float(trk["MinNs"]), "max_ns": float(trk["MaxNs"]), "counters": {}}
+# per-dispatch durations (the trace's first launch of a process runs cold:
+# caches, TLB and code are warmed by it, so it is reported apart)
+tr = os.path.join(base, f"{tag}_trace", "run_kernel_trace.csv")
+if os.path.exists(tr):
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) for r in csv.DictReader(open(tr))
+            if r["Kernel_Name"] == KNAME]
+    if len(durs) > 1:
+        warm = sorted(durs[1:])
+        out["first_dispatch_ns"] = durs[0]
+        out["warm_dispatches"] = len(warm)
+        out["warm_avg_ns"] = sum(warm) / len(warm)
+        out["warm_median_ns"] = warm[len(warm) // 2] if len(warm) % 2 else (warm[len(warm) // 2 - 1] + warm[len(warm) // 2]) / 2
 meta = None
 for d in sorted(glob.glob(os.path.join(base, f"{tag}_pmc*"))):
     f = os.path.join(d, "run_counter_collection.csv")
