@@ -15,13 +15,15 @@
 //    value); a maximum outside the fast reciprocal range (NaN, inf, zero,
 //    tiny, huge) or a tie in either half sends the step to the exact rare
 //    path (NaN at position I wins, first position among ties);
-//  * broadcast: the pivot lane writes its row (the non-zero column chunks),
-//    rhs and rowid into its half's LDS buffer (ds_write_b128), every lane
-//    reads it back (broadcast ds_read_b128);
-//  * 1/pivot: cuCdivf(1, pivot) with v_rcp_f32 + one Newton step, which is
-//    the IEEE quotient for s in [2^-90, 2^120) (exhaustively verified,
-//    scripts/rcp_check.hip, profiles/r1_rcp_check.json); the pivot lane keeps
-//    the factors (o1, o2) for the back substitution;
+//  * 1/pivot: every lane computes cuCdivf(1, a_rI) of its own candidate
+//    while the search runs (round 4: off the step's critical path), with
+//    v_rcp_f32 + one Newton step, which is the IEEE quotient for s in
+//    [2^-90, 2^120) (exhaustively verified, scripts/rcp_check.hip,
+//    profiles/r1_rcp_check.json); the pivot lane's is the step's 1/pivot, and
+//    it keeps the factors (o1, o2) for the back substitution;
+//  * broadcast: the pivot lane writes 1/pivot (in the pivot element's slot),
+//    its row (the non-zero column chunks), rhs and rowid into its half's LDS
+//    buffer (ds_write_b128), every lane reads it back (broadcast ds_read_b128);
 //  * one exec region (rows below the pivot): multiplier, right-hand side,
 //    fill-in pattern and the rank-1 update, 2 v_pk_fma_f32 per element.
 //
@@ -259,7 +261,7 @@ __device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pm
 // reports such a solve, and the caller solves the system again densely.
 template <int I, bool DENSE, int CH>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
-                                             bool is_piv, float piv_abs, int pl0, int pl1 HC_LU_WORK_ARG) {
+                                             bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s, bool elig HC_LU_WORK_ARG) {
     constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
     uint32_t pmw = FULL;
     if constexpr (!DENSE) {
@@ -270,38 +272,30 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     }
     const uint32_t gb = group_bits<CH>(pmw);
     HC_ISA_MARK_I("lu_store", I);
-    if (is_piv) {                                          // pivot row -> buffer
-        L.row[I] = rA[I];
+    if (is_piv) {                                          // pivot row -> buffer, 1/pivot in the pivot's slot
+        L.row[I] = cmk(reg_s.x, reg_s.y);
         lu_put_row<I, 0, CH>(rA, pmw, gb, L);
         L.row[30] = rB;
         L.row[31].x = __int_as_float(rowid);
     }
     wave_lds_sync();
     HC_ISA_MARK_I("lu_rcp", I);
-    const cf sxi = L.row[I];
+    const cf reg = L.row[I];
     cf sB0, pr;
     ld4(&L.row[30], sB0, pr);
     const int piv_pos = __float_as_int(pr.x);
     if (is_piv) rowid = I;                                 // :70-82
     else if (rowid == I) rowid = piv_pos;
-    // 1 / pivot as cuCdivf(1, pivot) (:84); the pivot lane keeps the factors
-    cf reg;
-    divf f;
-    if constexpr (!DENSE) {
-        pf2 oo;
-        const pf2 rg = recip_fast(pf2{sxi.x, sxi.y}, piv_abs, oo);
-        reg = cmk(rg.x, rg.y);
-        f.o1 = oo.x;
-        f.o2 = oo.y;
-    } else {
-        f = cdiv_factors(sxi);
-        reg = (piv_abs == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);   // :66
-    }
-    if (is_piv) my.oo = pf2{f.o1, f.o2};
+    // the pivot lane keeps its factors (computed in the search, lu_forward)
+    if (is_piv) my.oo = oo_s;
     // opaque: the select chain must be resolved here, not carried as 30
     // per-step factor pairs into the back substitution
     asm volatile("" : "+v"(my.oo));
-    const bool below = rowid > I;                          // :86-93
+    // :86-93: rowid > I after the relabel, i.e. an eligible row that is not the
+    // pivot (the displaced row takes the pivot's old id > I); known from the
+    // search, so the exec region does not wait for the read-back (padding lanes,
+    // never eligible, stay out: their rows are not part of the system)
+    const bool below = elig && !is_piv;
     // one exec-masked region per step: multiplier, right-hand side,
     // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
     // below whose column I may be non-zero takes the pivot patterns (both
@@ -327,6 +321,17 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
     if constexpr (I < NV) {
         HC_ISA_MARK_I("lu_search", I);
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
+        // 1 / own candidate as cuCdivf(1, a_rI) (:66, :84), off the step's critical path:
+        // the pivot lane's is the step's 1/pivot (same ops on the same value)
+        pf2 reg_s, oo_s;
+        if constexpr (!DENSE) {
+            reg_s = recip_fast(pf2{rA[I].x, rA[I].y}, v, oo_s);
+        } else {
+            const divf f = cdiv_factors(rA[I]);
+            const cf rg = (v == 0.0f) ? cmk(1.0f, 0.0f) : cdiv_apply(cmk(1.0f, 0.0f), f);
+            reg_s = pf2{rg.x, rg.y};
+            oo_s = pf2{f.o1, f.o2};
+        }
         const bool elig = rowid >= I && row_lane;
         bool is_piv;
         float piv_abs;
@@ -393,7 +398,7 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl1 = 32 + __builtin_ctz(mhi);
         }
         HC_ISA_MARK_I("lu_pattern", I);
-        lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, is_piv, piv_abs, pl0, pl1 HC_LU_WORK_PASS);
+        lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, is_piv, pl0, pl1, reg_s, oo_s, elig HC_LU_WORK_PASS);
         lu_forward<I + 1, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo HC_LU_WORK_PASS);
     }
 }
