@@ -97,8 +97,10 @@ def test_residual_gate_config2(problem, samples100, tracker):
 @pytest.mark.parametrize("inflight_stop", [0, 1])
 def test_abort_config3_N1000(problem, oracle, tracker, ransac0, inflight_stop):
     """Config 3 (1000 samples, abort on).  Found hypotheses pass the oracle's
-    scoring on their own (HIP == oracle) tracks; a sample of tracked paths and
-    every found path equal the oracle's tracks of the same batch ids; skipped
+    scoring on their own (HIP == oracle) tracks; every tracked path (round 4:
+    all of them, ~14 k with the reference's semantics, ~6 k with inflight_stop;
+    round 3 checked the found paths and a sample of 400) equals the oracle's
+    track of the same batch id; skipped
     (and, with inflight_stop, stopped) paths keep the start solution with conv 0
     and zero stats.  Reference semantics (inflight_stop 0): a path that started
     tracking writes its full result."""
@@ -112,9 +114,7 @@ def test_abort_config3_N1000(problem, oracle, tracker, ransac0, inflight_stop):
     st = r["stats"]
     tracked = st["steps"] > 0
     assert tracked[found].all() and (r["converge"][found] == 1).all()
-    rng = np.random.default_rng(inflight_stop)
-    tids = np.nonzero(tracked)[0]
-    check = np.unique(np.concatenate([found, rng.choice(tids, size=min(400, len(tids)), replace=False)]))
+    check = np.nonzero(tracked)[0]
     tr, conv, inf, ost = oracle.gpuhc_track_subset(check, problem.start_sols, problem.start_params, tgt, dif,
                                                    problem.unified_index)
     assert (r["converge"][check] == conv[check]).all() and (r["infinity"][check] == inf[check]).all()
