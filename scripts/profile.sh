@@ -3,7 +3,7 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 T=$1
-B="python bench.py --steps 8 --warmup 3 --no-cpu-baseline --abort-samples 0 --noisy-trials 0 --streams 1 --pipelined-streams 0"
+B="python bench.py --steps 30 --warmup 3 --no-cpu-baseline --abort-samples 0 --noisy-trials 0 --streams 1 --pipelined-streams 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${T}_trace -o run -- $B > gpurun_out/${T}_trace.log 2>&1; rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 i=0
 for set in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY" \
