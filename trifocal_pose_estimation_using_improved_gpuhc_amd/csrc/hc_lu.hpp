@@ -22,10 +22,11 @@
 //    profiles/r1_rcp_check.json); the pivot lane's is the step's 1/pivot, and
 //    it keeps the factors (o1, o2) for the back substitution;
 //  * broadcast: the pivot lane writes 1/pivot (in the pivot element's slot),
-//    its row (the non-zero column chunks), rhs and rowid into its half's LDS
-//    buffer (ds_write_b128), every lane reads it back (broadcast ds_read_b128);
-//  * one exec region (rows below the pivot): multiplier, right-hand side,
-//    fill-in pattern and the rank-1 update, 2 v_pk_fma_f32 per element.
+//    rhs and rowid into its half's LDS buffer, every lane reads them back;
+//  * rows below the pivot: multiplier, right-hand side and fill-in pattern;
+//  * per column group (one uniform test): the pivot lane writes the group of
+//    its row (ds_write_b128), the rows below read it back (broadcast
+//    ds_read_b128) and update, 2 v_pk_fma_f32 per element.
 //
 // Structural sparsity.  The trifocal Jacobian is sparse (170 of 900 entries
 // carry terms) and partial-pivot elimination fills it in only partly: on
@@ -184,25 +185,6 @@ __device__ __forceinline__ bool group_live(uint32_t pmw, uint32_t gb) {
     else return (gb >> J) & 1u;
 }
 
-// pivot lane: row elements of the groups of step I that are non-zero in some
-// pivot row of the wave
-template <int I, int K, int CH>
-__device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uint32_t gb, LUBuf &L) {
-    using C = LuChunks<CH>;
-    if constexpr (K < C::count(I)) {
-        constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
-            if constexpr (N == 1) {
-                L.row[J] = rA[J];
-            } else {
-#pragma unroll
-                for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
-            }
-        }
-        lu_put_row<I, K + 1, CH>(rA, pmw, gb, L);
-    }
-}
-
 #ifdef HC_DIAG_LUWORK
 // diagnostic build: rank-1 update elements the solves execute (sum over the
 // executed column groups of columns x active lanes), and the solves
@@ -223,34 +205,47 @@ struct LuWork { unsigned long long acc, mask, groups, rare; };   // mask: lanes 
 #define HC_LU_WORK_PASS
 #endif
 
-// a_j -= l * u_j for the groups K.. of step I (the caller is inside the
-// below-the-pivot exec region)
+// the column groups K.. of step I: one uniform test per group (round 4; the
+// pivot row's stores and the update each tested every group before: 2.2 %
+// faster, profiles/r4o_ab_fused_group_tests.jsonl); the pivot lanes write the
+// group, the rows below read it back and take a_j -= l * u_j
 template <int I, int K, int CH>
-__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, uint32_t gb,
-                                          const LUBuf &L HC_LU_WORK_ARG) {
+__device__ __forceinline__ void lu_store_update(cf (&rA)[NV], const cf &l, uint32_t pmw, uint32_t gb, LUBuf &L,
+                                                bool is_piv, bool below HC_LU_WORK_ARG) {
     using C = LuChunks<CH>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
         if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
-            HC_LU_WORK(N);
-#ifdef HC_DIAG_LUWORK
-            lu_work_acc.groups++;
-#endif
-            cf u[N];
-            if constexpr (N == 1) {
-                u[0] = L.row[J];
-            } else {
+            if (is_piv) {
+                if constexpr (N == 1) {
+                    L.row[J] = rA[J];
+                } else {
 #pragma unroll
-                for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
+                    for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
+                }
             }
+            wave_lds_sync();
+            if (below) {
+                HC_LU_WORK(N);
+#ifdef HC_DIAG_LUWORK
+                lu_work_acc.groups++;
+#endif
+                cf u[N];
+                if constexpr (N == 1) {
+                    u[0] = L.row[J];
+                } else {
 #pragma unroll
-            for (int q = 0; q < N; q++) {
-                const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
-                rA[J + q] = cmk(v.x, v.y);
+                    for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
+                }
+#pragma unroll
+                for (int q = 0; q < N; q++) {
+                    const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
+                    rA[J + q] = cmk(v.x, v.y);
+                }
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        lu_update<I, K + 1, CH>(rA, l, pmw, gb, L HC_LU_WORK_PASS);
+        lu_store_update<I, K + 1, CH>(rA, l, pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
     }
 }
 
@@ -274,7 +269,6 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     HC_ISA_MARK_I("lu_store", I);
     if (is_piv) {                                          // pivot row -> buffer, 1/pivot in the pivot's slot
         L.row[I] = cmk(reg_s.x, reg_s.y);
-        lu_put_row<I, 0, CH>(rA, pmw, gb, L);
         L.row[30] = rB;
         L.row[31].x = __int_as_float(rowid);
     }
@@ -300,16 +294,17 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
     // below whose column I may be non-zero takes the pivot patterns (both
     // halves': a superset of its own pivot row's).
+    pf2 lp = {0.0f, 0.0f};
     if (below) {
         HC_ISA_MARK_I("lu_mult", I);
-        const pf2 lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+        lp = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
         const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
         rB = cmk(bp.x, bp.y);
         // v_bfe_i32 + v_and_or_b32
         if constexpr (!DENSE) pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-        HC_ISA_MARK_I("lu_update", I);
-        lu_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
     }
+    HC_ISA_MARK_I("lu_update", I);
+    lu_store_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
 }
 
 // One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
