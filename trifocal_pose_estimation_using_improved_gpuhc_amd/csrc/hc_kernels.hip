@@ -1824,7 +1824,7 @@ int hc_trifocal_abi_version(void) { return HC_TRIFOCAL_ABI_VERSION; }
 void hc_trifocal_set_ring_test(int delay_ticks) { hc::g_ring_test = delay_ticks > 0 ? delay_ticks : 0; }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.7 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
+    return "hc_trifocal gfx950 v9.8 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
            "readlane back substitution, pipelined evals over per-slot prefix tables, 5 waves/SIMD, time slicing "
            "at step boundaries with least-attained-service issue priority)";
 }

@@ -185,6 +185,25 @@ __device__ __forceinline__ bool group_live(uint32_t pmw, uint32_t gb) {
     else return (gb >> J) & 1u;
 }
 
+// pivot lane: row elements of the groups of step I that are non-zero in some
+// pivot row of the wave
+template <int I, int K, int CH>
+__device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uint32_t gb, LUBuf &L) {
+    using C = LuChunks<CH>;
+    if constexpr (K < C::count(I)) {
+        constexpr int J = C::start(I, K), N = C::len(I, K);
+        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
+            if constexpr (N == 1) {
+                L.row[J] = rA[J];
+            } else {
+#pragma unroll
+                for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
+            }
+        }
+        lu_put_row<I, K + 1, CH>(rA, pmw, gb, L);
+    }
+}
+
 #ifdef HC_DIAG_LUWORK
 // diagnostic build: rank-1 update elements the solves execute (sum over the
 // executed column groups of columns x active lanes), and the solves
@@ -204,6 +223,37 @@ struct LuWork { unsigned long long acc, mask, groups, rare; };   // mask: lanes 
 #define HC_LU_WORK_ARG
 #define HC_LU_WORK_PASS
 #endif
+
+// a_j -= l * u_j for the groups K.. of step I (the caller is inside the
+// below-the-pivot exec region)
+template <int I, int K, int CH>
+__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, uint32_t gb,
+                                          const LUBuf &L HC_LU_WORK_ARG) {
+    using C = LuChunks<CH>;
+    if constexpr (K < C::count(I)) {
+        constexpr int J = C::start(I, K), N = C::len(I, K);
+        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
+            HC_LU_WORK(N);
+#ifdef HC_DIAG_LUWORK
+            lu_work_acc.groups++;
+#endif
+            cf u[N];
+            if constexpr (N == 1) {
+                u[0] = L.row[J];
+            } else {
+#pragma unroll
+                for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
+            }
+#pragma unroll
+            for (int q = 0; q < N; q++) {
+                const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
+                rA[J + q] = cmk(v.x, v.y);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        lu_update<I, K + 1, CH>(rA, l, pmw, gb, L HC_LU_WORK_PASS);
+    }
+}
 
 // the column groups K.. of step I: one uniform test per group (round 4; the
 // pivot row's stores and the update each tested every group before: 2.2 %
@@ -269,6 +319,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     HC_ISA_MARK_I("lu_store", I);
     if (is_piv) {                                          // pivot row -> buffer, 1/pivot in the pivot's slot
         L.row[I] = cmk(reg_s.x, reg_s.y);
+        if constexpr (CH != 2) lu_put_row<I, 0, CH>(rA, pmw, gb, L);
         L.row[30] = rB;
         L.row[31].x = __int_as_float(rowid);
     }
@@ -304,7 +355,15 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         if constexpr (!DENSE) pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
     }
     HC_ISA_MARK_I("lu_update", I);
-    lu_store_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
+    // the tracking kernels (groups of 2) test each group once for the store and
+    // the update; the abort kernel (groups of 4, latency: its time to the first
+    // pose) keeps the two loops, whose stores all issue before the first
+    // update reads (profiles/r4q_ttfp_abort_structure.jsonl)
+    if constexpr (CH == 2) {
+        lu_store_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
+    } else if (below) {
+        lu_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
+    }
 }
 
 // One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
