@@ -118,16 +118,81 @@ def parse():
     return ap.parse_args()
 
 
+SCHEMA = 5   # bench-line schema: bumped when a field changes meaning (roofline.achieved is dense-priced since 4)
+
+
+def launch_plan(gpus, environ):
+    """How this process runs `--gpus N`: ("single", 1) for N = 1
+    without a launcher; ("rank", N) when a launcher (torch.distributed.run) set
+    WORLD_SIZE = N; ("spawn", N) for N > 1 without one: bench.py starts the N
+    ranks itself (spawn_command) before anything touches the GPU.  A launcher
+    whose WORLD_SIZE differs from --gpus is an error, never a silent N = 1 run."""
+    if gpus < 1:
+        raise SystemExit(f"[bench] --gpus must be >= 1 (got {gpus})")
+    ws = environ.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        return ("single", 1) if gpus == 1 else ("spawn", gpus)
+    try:
+        world = int(ws)
+    except ValueError:
+        raise SystemExit(f"[bench] WORLD_SIZE={ws!r} is not an integer")
+    if world != gpus:
+        raise SystemExit(f"[bench] --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+    return ("rank", world) if world > 1 else ("single", 1)
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_command(gpus, argv, port):
+    """The child that runs the N ranks: torch.distributed.run on 127.0.0.1, one
+    process per GPU (LOCAL_RANK = device), this script with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus, argv):
+    """Runs the ranks as a child process (never an exec: this process has not
+    touched the GPU, and the ranks are fresh processes) and returns its exit
+    code; non-zero when any rank failed to start or run."""
+    import subprocess
+    env = dict(os.environ, HC_BENCH_SPAWNED="1")
+    try:
+        return subprocess.run(spawn_command(gpus, argv, free_port()), env=env).returncode or 0
+    except OSError as e:
+        print(f"[bench] could not start {gpus} ranks: {e}", file=sys.stderr)
+        return 1
+
+
+def gather_floats(vals, dev, world):
+    """Every rank's list of floats (same length on every rank), rank-ordered."""
+    if world == 1:
+        return [list(vals)]
+    import torch
+    import torch.distributed as dist
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    t = torch.tensor([float(v) for v in vals], dtype=torch.float64, device=on)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t)
+    return [p.cpu().tolist() for p in parts]
+
+
 def main():
     args = parse()
+    mode, world = launch_plan(args.gpus, os.environ)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
     # rehearsal of the N>1 path on a one-GPU box (never set by the driver):
     # HC_BENCH_DEVICE pins every rank to one device, HC_BENCH_BACKEND=gloo
     # replaces RCCL (which refuses two ranks on one GPU)
@@ -135,11 +200,15 @@ def main():
     backend = os.environ.get("HC_BENCH_BACKEND", "nccl")
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
+    dist_world = 1
     if world > 1:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
+        dist_world = dist.get_world_size()
+        if dist_world != args.gpus:
+            raise SystemExit(f"[bench] --gpus {args.gpus} but the process group has {dist_world} ranks")
 
     from trifocal_pose_estimation_using_improved_gpuhc_amd import (_abi, load_problem, load_ransac_data,
                                                                    prepare_target_params)
@@ -188,6 +257,8 @@ def main():
         for i in range(args.steps):
             step(i, ns, strs)
         torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0          # this rank's own time (before the barrier)
+        own.setdefault(ns, el)
         if world > 1:
             dist.barrier()
         el = time.perf_counter() - t0
@@ -206,7 +277,9 @@ def main():
             el = float(tt.item())
         return el
 
+    own = {}
     elapsed = timed(NS, streams)
+    el_own = own[NS]
     pipe_elapsed = timed(args.pipelined_streams, pstreams) if args.pipelined_streams > 1 else None
 
     # kernel time of one launch alone (serial, HIP events on the launch stream): the
@@ -220,6 +293,8 @@ def main():
     torch.cuda.synchronize(dev)
     tr.workspace_status()   # raises on a device-side failure (table / time-slicing hand-over)
     launch_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
+    # every rank's own kernel time (median of its 5 single launches) and wall time per step
+    rank_ms = gather_floats([float(np.median(launch_ms)), el_own * 1e3 / args.steps], dev, world)
 
     # the papers' ablation ladder: the same launch through the archived
     # ..._PH (explicit RK, no truncation) and ..._PH_CodeOpt (no truncation) semantics
@@ -298,8 +373,10 @@ def main():
             abort_info["cross_rank_stop"] = ("device flag over xGMI (hipIpc) + RCCL all_reduce at chunk boundaries"
                                              if peer.ptr is not None else
                                              f"RCCL all_reduce at chunk boundaries only ({peer.error})")
+        n_chunks = len(sharding.chunks(cnt, args.abort_chunk))
         for inflight in (False, True):
             ttfp, wall, tracked = [], [], []
+            found_runs, per_rank_runs = [], []
             for _ in range(args.abort_repeats):
                 tr.reset_tracks(ra)
                 torch.cuda.synchronize(dev)
@@ -314,9 +391,16 @@ def main():
                 torch.cuda.synchronize(dev)
                 w = time.perf_counter() - w0
                 hz = tr.read_timestamps(wss[0])[2]
-                f = sharding.first_found_seconds([tr.read_timestamps(x)[:2]
-                                                  for x in wss[:len(sharding.chunks(cnt, args.abort_chunk))]], hz)
+                stamps = [tr.read_timestamps(x)[:2] for x in wss[:n_chunks]]
+                f = sharding.first_found_seconds(stamps, hz)
                 n_tr = int((ra.stats[:, 0] > 0).sum().item())
+                # per rank: did it find a pose itself (a found stamp in one of its own
+                # launches), how many of its shard's paths it tracked, and the found
+                # byte it ended with (its own find, the peer flag or the chunk reduction)
+                self_found = any(fs for _, fs in stamps)
+                per_rank_runs.append(gather_floats([1.0 if self_found else 0.0, float(n_tr),
+                                                    float(bool(ra.found.item()))], dev, world))
+                found_runs.append(bool(ra.found.item()))
                 if world > 1:
                     v = torch.tensor([f if f >= 0 else 1e30, -w, -float(n_tr)], dtype=torch.float64, device=dev)
                     dist.all_reduce(v, op=dist.ReduceOp.MIN)
@@ -328,17 +412,36 @@ def main():
                 ttfp.append(f)
                 wall.append(w)
                 tracked.append(n_tr)
-            found = bool(ra.found.item())
             key = "inflight_stop" if inflight else "reference_semantics"
             ok = [f for f in ttfp if f >= 0]
             spread = lambda v: {"median": round(float(np.median(v)) * 1e3, 3),  # noqa: E731
                                 "min": round(float(np.min(v)) * 1e3, 3), "max": round(float(np.max(v)) * 1e3, 3)}
+            shards = [sharding.shard(Sa * world, world, g)[1] * 312 for g in range(world)]
+            chunk_paths = args.abort_chunk * 312
+            ranks = []
+            for g in range(world):
+                runs = [pr[g] for pr in per_rank_runs]
+                tr_g = [int(x[1]) for x in runs]
+                # a rank that found nothing itself and tracked fewer paths than its
+                # shard was stopped by another rank's find; mid-launch when the count
+                # is not a whole number of chunks (the chunk-boundary reduction
+                # stops only between chunks, the device flag inside a launch)
+                peer = [not x[0] and int(x[1]) < shards[g] for x in runs]
+                mid = [p and int(x[1]) % chunk_paths != 0 for p, x in zip(peer, runs)]
+                ranks.append({"rank": g, "shard_paths": shards[g],
+                              "self_found_runs": int(sum(1 for x in runs if x[0])),
+                              "paths_tracked": {"median": int(np.median(tr_g)), "min": min(tr_g), "max": max(tr_g)},
+                              "peer_stopped_runs": int(sum(peer)), "peer_stopped_mid_launch_runs": int(sum(mid))})
             abort_info[key] = {
-                "found": found,
+                "found": all(found_runs),
+                "found_runs": int(sum(found_runs)),
                 "runs": len(ttfp),
                 "time_to_first_good_pose_ms": spread(ok) if ok else None,
                 "kernel_exit_wall_ms": spread(wall),
-                "paths_tracked": int(np.median(tracked))}
+                "paths_tracked": int(np.median(tracked)),
+                "per_rank": ranks,
+                "peer_stop_observed": any(r_["peer_stopped_runs"] > 0 for r_ in ranks),
+                "peer_stop_mid_launch_observed": any(r_["peer_stopped_mid_launch_runs"] > 0 for r_ in ranks)}
         if peer is not None:
             peer.close()
         abort_info["note"] = ("device clock (s_memrealtime, rate from hipDeviceAttributeWallClockRate) from the "
@@ -356,14 +459,31 @@ def main():
         achieved_tf = flops / med_launch_s / 1e12                  # the reference's (dense) LU
         achieved_exec_tf = None if flops_exec is None else flops_exec / med_launch_s / 1e12
         traffic, traffic_src = traffic_bytes(TRACK_KERNEL, bid)
+        alg_bytes = algorithmic_bytes(S)
+        k_ms = [r_[0] for r_ in rank_ms]
         line = {
             "metric": "HC paths/sec (312 tracks x RANSAC samples)",
             "value": round(value, 1),
             "unit": "paths/s",
             "n_gpus": world,
+            "world_size": dist_world,
+            "schema": SCHEMA,
+            "distributed": {
+                "launcher": ("bench.py (torch.distributed.run child it started)" if os.environ.get("HC_BENCH_SPAWNED")
+                             else "external (WORLD_SIZE set)") if world > 1 else "none (one process)",
+                "backend": dist.get_backend() if world > 1 else None,
+                "world_size_reported_by": "torch.distributed.get_world_size()" if world > 1 else None,
+                "devices": ("all ranks on cuda:%d (rehearsal)" % dev_idx) if "HC_BENCH_DEVICE" in os.environ
+                           else "cuda:LOCAL_RANK",
+                "per_rank_kernel_ms": [round(v, 4) for v in k_ms],
+                "kernel_ms_min": round(min(k_ms), 4), "kernel_ms_max": round(max(k_ms), 4),
+                "per_rank_step_ms": [round(r_[1], 4) for r_ in rank_ms],
+                "note": "kernel ms = median of each rank's 5 single config-2 launches (HIP events); step ms = "
+                        "the rank's own timed-loop time per step before the closing barrier; ms_per_step is "
+                        "the max over ranks after it"},
+            "ms_per_step": round(ms_per_step, 4),
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -392,9 +512,19 @@ def main():
                          "unit": "TFLOP/s", "frac": round(achieved_tf / FP32_PEAK_TFLOPS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src,
+                         # north_star's "achieved HBM GB/s fraction from rocprof" (VERDICT r4 #2):
+                         # the PMC bytes of this build over this run's kernel time
+                         "hbm_gbs": None if traffic is None else round(traffic / (float(np.median(launch_ms)) / 1e3) / 1e9, 3),
+                         "hbm_frac": None if traffic is None else
+                         round(traffic / (float(np.median(launch_ms)) / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
+                         "hbm_peak_gbs": HBM_PEAK_GBS,
+                         "algorithmic_bytes": alg_bytes,
+                         "algorithmic_gbs": round(alg_bytes / (float(np.median(launch_ms)) / 1e3) / 1e9, 3),
+                         "traffic_over_algorithmic": None if traffic is None else round(traffic / alg_bytes, 3),
                          "traffic_unit": "HBM bytes per launch of the same kernel (rocprofv3 FETCH_SIZE x2 gfx950 "
                                          "correction + WRITE_SIZE, separate --pmc passes, scripts/profile.sh); "
-                                         "algorithmic ~0.5 KB/path = 15.3 MB/launch",
+                                         "algorithmic_bytes: the compulsory bytes of the same launch (bench.algorithmic_bytes, ~0.5 KB/path); "
+                                         "hbm_gbs / hbm_frac: traffic / this run's median kernel time, / 8 TB/s",
                          "note": "FP32 VALU-issue/latency bound tracker kernel (no GEMM: 30x30 complex LUs of "
                                  "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = algorithmic "
                                  "FLOPs of the launch's stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 "
@@ -506,6 +636,15 @@ def noisy_pose_leg(args, tr, problem, data, world, rank, dev, stream):
             "paths_per_s": round(312 * S * world * args.noisy_trials / tt, 1),
             "ms_per_run": round(tt / args.noisy_trials * 1e3, 3),
             "median_candidates": int(np.median(cands))}
+
+
+def algorithmic_bytes(samples):
+    """Compulsory HBM bytes of one config-2 launch over `samples` samples (SURVEY
+    §8(d)): per path the 31-entry start / track row read (248 B), the
+    30 solved entries written back (240 B), converge + infinity (2 B) and the
+    stats record (16 B); per sample the target and diff parameters (2 x 34 c64);
+    per launch the unified index table (38 880 int32) and the start parameters."""
+    return 312 * samples * (31 * 8 + 30 * 8 + 2 + 16) + samples * 2 * 34 * 8 + 38880 * 4 + 34 * 8
 
 
 def traffic_bytes(kernel, bid):

@@ -104,6 +104,7 @@ private:
     bool Abort_Inflight_Stop = false;   // not in the reference: hcAbortArgs::inflight_stop
     bool Abort_Across_GPUs = false;     // not in the reference: one found flag for all GPUs (hcAbortArgs::peer_found)
     uint32_t *d_peer_found = nullptr;   // on the first GPU's device, read and set by every GPU's launch
+    const char *peer_flag_kind_ = nullptr;   // memory the flag got: "uncached", "fine-grained" or "coarse-grained (hipMalloc)"
     int Pose_Flags = 0;   // Pose_Selection_Reference_Quirks -> HC_POSE_REFERENCE_QUIRKS
     int Num_Of_GPUs = 1;
     int Num_Of_RANSAC_Iterations = 100;   // NUM_OF_RANSAC_ITERATIONS (definitions.hpp:12), runtime here

@@ -266,12 +266,6 @@ const char *hc_trifocal_version(void);
 #define HC_TRIFOCAL_ABI_VERSION 2
 int hc_trifocal_abi_version(void);
 
-/* Tests only: every 16th ring ticket of later sliced launches in this process
-   waits delay_ticks (device clock ticks, 100 MHz) between its ticket and its
-   entry, and consumers abandon a ticket after delay_ticks / 8 instead of 1 ms,
-   so that the abandon / re-push hand-over runs; 0 restores the default. */
-void hc_trifocal_set_ring_test(int delay_ticks);
-
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,24 @@
+/* hc_trifocal_testing.h -- test hooks of libhc_trifocal.so, apart from the
+   public ABI (include/hc_trifocal.h) so that no product caller binds them
+   (ADVICE r4).  No reference counterpart. */
+#ifndef HC_TRIFOCAL_TESTING_H
+#define HC_TRIFOCAL_TESTING_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Every 16th ring ticket of later sliced launches in this process waits
+   delay_ticks (device clock ticks, 100 MHz) between its ticket and its entry,
+   and consumers abandon a ticket after delay_ticks / 8 instead of 1 ms, so that
+   the abandon / re-push hand-over of time slicing runs.  0 (or a negative
+   value) restores the default; positive values are raised to at least
+   HC_RING_TEST_MIN_TICKS, so that consumers wait a few hundred ticks and a
+   stray call cannot make them abandon every ticket.  Read at launch time. */
+#define HC_RING_TEST_MIN_TICKS 4096
+void hc_trifocal_set_ring_test(int delay_ticks);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HC_TRIFOCAL_TESTING_H */

@@ -273,10 +273,24 @@ void GPU_HC_Solver::Set_RANSAC_Abort_Arrays() {
             (void)hipGetLastError();
         }
         HC_HIP_CHECK(hipSetDevice(dev0));
-        if (hipExtMallocWithFlags((void **)&d_peer_found, 256, hipDeviceMallocUncached) != hipSuccess) {
-            (void)hipGetLastError();
-            HC_HIP_CHECK(hipExtMallocWithFlags((void **)&d_peer_found, 256, hipDeviceMallocFinegrained));
+        // the same order as hc_shared_flag_create: uncached, fine-grained, then
+        // plain memory as the last resort (said once on stderr)
+        static const char *const kind_name[3] = {"uncached", "fine-grained", "coarse-grained (hipMalloc)"};
+        hipError_t e = hipErrorOutOfMemory;
+        for (int k = 0; k < 3 && !d_peer_found; k++) {
+            e = k == 0 ? hipExtMallocWithFlags((void **)&d_peer_found, 256, hipDeviceMallocUncached)
+              : k == 1 ? hipExtMallocWithFlags((void **)&d_peer_found, 256, hipDeviceMallocFinegrained)
+                       : hipMalloc((void **)&d_peer_found, 256);
+            if (e != hipSuccess) {
+                (void)hipGetLastError();
+                d_peer_found = nullptr;
+                continue;
+            }
+            peer_flag_kind_ = kind_name[k];
+            if (k > 0)
+                fprintf(stderr, "[GPU_HC_Solver] Abort_Across_GPUs: the found flag is in %s memory\n", kind_name[k]);
         }
+        HC_HIP_CHECK(e);
         HC_HIP_CHECK(hipMemset(d_peer_found, 0, 256));
     }
 }

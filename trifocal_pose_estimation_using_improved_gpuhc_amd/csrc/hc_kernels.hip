@@ -16,7 +16,10 @@
 #include "hc_device.hpp"
 #include "hc_lu.hpp"
 #include "../../include/hc_trifocal.h"
+#include "../../include/hc_trifocal_testing.h"
 
+#include <atomic>
+#include <climits>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -1465,6 +1468,22 @@ __global__ void __launch_bounds__(WG_THREADS) k_eval(int n, const Workspace *ws,
     }
 }
 
+// Epilogue of a sliced launch: once the tracker has drained, every
+// pushed ring entry has been taken (head == tail) and every unpaired push
+// claimed (avail == 0).  Otherwise a suspended path was never resumed and its
+// outputs are stale: HC_ERROR_DEVICE (hc_trifocal_workspace_status), with
+// (~0, avail, tail, head) in ring_fail.  One thread, stream-ordered after k_track.
+__global__ void __launch_bounds__(64) k_ring_check(Workspace *ws, const unsigned *rq) {
+    if (threadIdx.x != 0) return;
+    const unsigned head = ld_rlx(&rq[RQ_HEAD]), tail = ld_rlx(&rq[RQ_TAIL]), avail = ld_rlx(&rq[RQ_AVAIL]);
+    if ((head != tail || avail != 0u) && atomicMax(&ws->status, (unsigned)HC_ERROR_DEVICE) == 0u) {
+        ws->ring_fail[0] = 0xFFFFFFFFu;
+        ws->ring_fail[1] = avail;
+        ws->ring_fail[2] = tail;
+        ws->ring_fail[3] = head;
+    }
+}
+
 // ---------------------------------------------------------------- host side
 static size_t ws_bytes_needed() { return (sizeof(Workspace) + 255) & ~(size_t)255; }
 // + the time-slicing area of a launch of `paths` paths: the ring counters, the
@@ -1481,8 +1500,9 @@ static size_t ws_bytes_for(long long paths, int max_steps) {
     return ws_bytes_needed() + RQ_WORDS * sizeof(unsigned) + ring_bytes(ring_entries(paths, max_steps)) +
            (size_t)paths * SUSP_WORDS * sizeof(unsigned long long);
 }
-// tests only (hc_trifocal_set_ring_test): pusher delay of every 16th ring ticket
-static int g_ring_test = 0;
+// tests only (hc_trifocal_set_ring_test, include/hc_trifocal_testing.h): pusher
+// delay of every 16th ring ticket; read by every launch of every thread
+static std::atomic<int> g_ring_test{0};
 
 // Persistent grid: resident workgroups (occupancy API, cached per device and
 // kernel) x CUs, capped by the work.
@@ -1549,8 +1569,11 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     k.ws = ws;
     // time slicing when the workspace has room for it (hc_trifocal_workspace_size_for) and
     // the step counters fit the suspend block
+    // (the suspend blocks' span in ring-entry units, PrepArgs::susp_entry1, is a
+    // 32-bit word: slicing only where it fits)
+    const size_t susp_end = ring_bytes(ring_entries(paths, t->settings.max_steps)) / 8 + (size_t)paths * SUSP_WORDS;
     if (!abort_mode && SLICE_Q > 0 && wsb >= ws_bytes_for(paths, t->settings.max_steps) &&
-        ring_entries(paths, t->settings.max_steps) < 0xFFFFFF00ull &&
+        ring_entries(paths, t->settings.max_steps) < 0xFFFFFF00ull && susp_end < (size_t)UINT_MAX &&
         slice_fits(t->settings.max_steps, t->settings.max_corrections, t->settings.delta_t_inc_steps)) {
         char *base = (char *)workspace + ws_bytes_needed();
         k.ring_cap = (unsigned)ring_entries(paths, t->settings.max_steps);
@@ -1558,13 +1581,13 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
         k.ring = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned));
         k.susp = (unsigned long long *)(base + RQ_WORDS * sizeof(unsigned) + ring_bytes(k.ring_cap));
         k.slice_q = SLICE_Q;
-        k.ring_test = g_ring_test;
+        k.ring_test = g_ring_test.load(std::memory_order_relaxed);
     }
     // control block reset, compacted tables (skipped when cached), ring reset
     PrepArgs pa{t->unified_index, ws, abort_mode ? ab->found_trifocal_sols : nullptr,
                 abort_mode ? ab->peer_found : nullptr, k.rq, k.ring, k.ring_cap,
                 k.rq ? (unsigned)(ring_bytes(k.ring_cap) / 8) : 0u,
-                k.rq ? (unsigned)(ring_bytes(k.ring_cap) / 8 + (size_t)paths * SUSP_WORDS) : 0u};
+                k.rq ? (unsigned)susp_end : 0u};
     hipLaunchKernelGGL(k_prep_tables, dim3(1), dim3(PREP_THREADS), 0, s, pa);
     if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     // tracking: term tables read from the workspace (L1/L2), 96 VGPRs, 27.6 KB LDS
@@ -1589,7 +1612,12 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     void *kargs[] = {&k};
     g_last_hip_error = hipLaunchKernel(kern, dim3(grid), dim3(WG_THREADS), kargs, 0, s);
     if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
-    return launch_status(HC_ERROR_LAUNCH);
+    if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
+    if (k.rq) {   // a suspended path that was never resumed is reported, not left stale
+        hipLaunchKernelGGL(k_ring_check, dim3(1), dim3(64), 0, s, ws, (const unsigned *)k.rq);
+        return launch_status(HC_ERROR_LAUNCH);
+    }
+    return HC_SUCCESS;
 }
 
 static hcStatus read_control(const void *workspace, Workspace &h) {
@@ -1821,7 +1849,11 @@ int hc_diag_util(unsigned long long *out, int reset) {
 
 int hc_trifocal_abi_version(void) { return HC_TRIFOCAL_ABI_VERSION; }
 
-void hc_trifocal_set_ring_test(int delay_ticks) { hc::g_ring_test = delay_ticks > 0 ? delay_ticks : 0; }
+void hc_trifocal_set_ring_test(int delay_ticks) {
+    hc::g_ring_test.store(delay_ticks > 0 ? (delay_ticks < HC_RING_TEST_MIN_TICKS ? HC_RING_TEST_MIN_TICKS : delay_ticks)
+                                          : 0,
+                          std::memory_order_relaxed);
+}
 
 const char *hc_trifocal_version(void) {
     return "hc_trifocal gfx950 v9.8 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
