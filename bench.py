@@ -426,12 +426,12 @@ def main():
                 # shard was stopped by another rank's find; mid-launch when the count
                 # is not a whole number of chunks (the chunk-boundary reduction
                 # stops only between chunks, the device flag inside a launch)
-                peer = [not x[0] and int(x[1]) < shards[g] for x in runs]
-                mid = [p and int(x[1]) % chunk_paths != 0 for p, x in zip(peer, runs)]
+                pstop = [not x[0] and int(x[1]) < shards[g] for x in runs]
+                mid = [p and int(x[1]) % chunk_paths != 0 for p, x in zip(pstop, runs)]
                 ranks.append({"rank": g, "shard_paths": shards[g],
                               "self_found_runs": int(sum(1 for x in runs if x[0])),
                               "paths_tracked": {"median": int(np.median(tr_g)), "min": min(tr_g), "max": max(tr_g)},
-                              "peer_stopped_runs": int(sum(peer)), "peer_stopped_mid_launch_runs": int(sum(mid))})
+                              "peer_stopped_runs": int(sum(pstop)), "peer_stopped_mid_launch_runs": int(sum(mid))})
             abort_info[key] = {
                 "found": all(found_runs),
                 "found_runs": int(sum(found_runs)),
