@@ -2,4 +2,4 @@
 # update (v3) against the round-4 LU (base) and the eligible-rows groups (v1)
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-bash scripts/gpu_ab.sh r5d base=lib/libhc_trifocal_r5base.so v1=lib/libhc_trifocal_v1.so v3=lib/libhc_trifocal_v3.so
+bash scripts/gpu_ab.sh ${T:-r5d} base=lib/libhc_trifocal_r5base.so v1=lib/libhc_trifocal_v1.so v3=lib/libhc_trifocal_v3.so v4=lib/libhc_trifocal_v4.so

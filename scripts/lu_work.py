@@ -38,8 +38,15 @@ def main():
     out = (C.c_ulonglong * 10)()
     dev = torch.device("cuda:0")
     problem = load_problem()
-    tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, 100)
-    scaled = "--scaled" in sys.argv[1:]
+    argv = sys.argv[1:]
+    ds = int(argv[argv.index("--dataset") + 1]) if "--dataset" in argv else 0
+    seed = int(argv[argv.index("--seed") + 1]) if "--seed" in argv else 0
+    data = load_ransac_data(ds)
+    if "--sigma" in argv:   # noisy synthcurves of the dataset (trifocal_..._amd/synthcurves.py)
+        from trifocal_pose_estimation_using_improved_gpuhc_amd import synthcurves
+        data = synthcurves.noisy(data, float(argv[argv.index("--sigma") + 1]), synthcurves.DEFAULT_SEED)
+    tgt, dif, _ = prepare_target_params(problem, data, seed, 100)
+    scaled = "--scaled" in argv
     if scaled:
         tgt = np.stack([tgt[0]] + [(tgt[0] * np.float32(s)).astype(np.float32) for s in (2.0 ** 40, 2.0 ** 70)])
         dif = (tgt - problem.start_params[None]).astype(np.float32)
@@ -59,7 +66,10 @@ def main():
     wsolves, groups, rare = int(out[3]), int(out[4]), int(out[5])
     ev = [int(out[6]), int(out[7]), int(out[8])]
     res = {"config": ("sample 0 of config 2 + its target params x 2^40, x 2^70 (one launch)" if scaled
-                      else "config 2 (100 samples, abort off), one launch"),
+                      else "config 2 (100 samples, abort off), one launch" +
+                      ("" if (ds, seed) == (0, 0) and "--sigma" not in argv else
+                       f", dataset {ds:03d}, srand({seed})" + (f", sigma {argv[argv.index('--sigma') + 1]} px"
+                                                              if "--sigma" in argv else ""))),
            "sparse_solves_completed": solves, "path_stages": stages,
            "solves_rerun_densely": dense,
            "check": "sparse_solves_completed + solves_rerun_densely == path_stages",

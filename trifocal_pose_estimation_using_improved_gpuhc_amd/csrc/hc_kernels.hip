@@ -1257,17 +1257,20 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         HC_DIAG_MARK(2);
         bool redo;
         LUBuf &LB = *reinterpret_cast<LUBuf *>(S.lu);
+        // the LU's scratch: the dH/dx entry block, dead once gathered into rA
+        // (a dense re-solve evaluates dH/dx again)
+        static_assert(ENT_CAP >= LU_SCRATCH_CF && offsetof(SlotLDS, ent) % 16 == 0, "LU scratch in SlotLDS::ent");
 #ifdef HC_DIAG_LUWORK
-        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, redo, __ballot(act));   // :188 / :224
+        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, S.ent, redo, __ballot(act));   // :188 / :224
 #else
-        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, redo);                  // :188 / :224
+        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, S.ent, redo);                  // :188 / :224
 #endif
         HC_ISA_MARK("ctl_redo");
         if (__builtin_expect(redo, 0)) {
             // a system the sparse solve cannot take exactly (an entry not provably
-            // finite, a pivot outside the fast reciprocal range): the Jacobian is
-            // re-gathered from the entry block (which the solve leaves intact),
-            // the right-hand side re-evaluated, and the system solved densely
+            // finite, a pivot outside the fast reciprocal range): dH/dx and the
+            // right-hand side are evaluated again (the sparse solve used the
+            // entry block as its scratch), and the system solved densely
             // (the stage kind re-read from the parked slot state: held across the
             // LU, act / pred would be spilled)
             HC_ISA_MARK("redo_evals");
@@ -1281,11 +1284,12 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                 const cf t = eval_rhs<RHS_H>(s_ht, S, r_v, false, rhs_masks(T));
                 if (!pred_r) rb = t;
             }
-            gather_hx(rA, &s_rowc[0][0], S, r_v);
+            eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_v);
+            wave_lds_sync();
 #ifdef HC_DIAG_LUWORK
-            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, redo, __ballot(act_r));
+            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, S.ent, redo, __ballot(act_r));
 #else
-            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, redo);
+            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, S.ent, redo);
 #endif
         }
         wave_lds_sync();
@@ -1395,6 +1399,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restrict__ A, const cf *__restrict__ B,
                                                       cf *__restrict__ X) {
     __shared__ LUBuf s_lu[2 * WAVES_PER_WG];
+    __shared__ __attribute__((aligned(16))) cf s_scr[2 * WAVES_PER_WG][LU_SCRATCH_CF];
     const int lane = lane_id();
     const int r = lane & 31;
     const int sys = (blockIdx.x * WAVES_PER_WG + threadIdx.x / WAVE) * 2 + (lane >> 5);
@@ -1408,12 +1413,13 @@ __global__ void __launch_bounds__(WG_THREADS) k_cgesv(int n, const cf *__restric
     }
     const cf rB = ok ? B[(size_t)sys * NV + r] : cmk(0.0f, 0.0f);
     LUBuf &LB = s_lu[(threadIdx.x / WAVE) * 2 + (lane >> 5)];
+    cf *scr = s_scr[(threadIdx.x / WAVE) * 2 + (lane >> 5)];
     bool redo;
-    cf x = lu_solve<false>(rA, rB, lane, pat, LB, redo, __ballot(sys < n));
+    cf x = lu_solve<false>(rA, rB, lane, pat, LB, scr, redo, __ballot(sys < n));
     if (__builtin_expect(redo, 0)) {   // solved again densely from the original system
 #pragma unroll
         for (int c = 0; c < NV; c++) rA[c] = ok ? A[((size_t)sys * NV + r) * NV + c] : cmk(0.0f, 0.0f);
-        x = lu_solve<true>(rA, rB, lane, pat, LB, redo);
+        x = lu_solve<true>(rA, rB, lane, pat, LB, scr, redo);
     }
     if (ok) X[(size_t)sys * NV + r] = x;
 }

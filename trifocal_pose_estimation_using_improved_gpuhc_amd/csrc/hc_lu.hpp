@@ -213,9 +213,10 @@ __device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uin
 // H-only evaluation, [9] stages that rebuilt the prefix tables (k_track)
 constexpr int DIAG_LUWORK_WORDS = 10;
 __device__ unsigned long long g_diag_luwork[DIAG_LUWORK_WORDS];
-struct LuWork { unsigned long long acc, mask, groups, rare; };   // mask: lanes whose work counts (active path slots)
+struct LuWork { unsigned long long acc, mask, groups, rare, excl; };   // mask: lanes whose work counts (active
+                                                                      // path slots); excl: lanes that update by l = 0
 #define HC_LU_WORK(ncols) (lu_work_acc.acc += (unsigned long long)(ncols) * \
-    (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask))
+    (unsigned long long)__builtin_popcountll(__builtin_amdgcn_read_exec() & lu_work_acc.mask & ~lu_work_acc.excl))
 #define HC_LU_WORK_ARG , LuWork &lu_work_acc
 #define HC_LU_WORK_PASS , lu_work_acc
 #else
@@ -299,6 +300,58 @@ __device__ __forceinline__ void lu_store_update(cf (&rA)[NV], const cf &l, uint3
     }
 }
 
+// The column groups K.. of step I inside the eligible rows' exec region (the
+// rows below and the pivot row; round 5): one uniform test per group, then
+// every eligible lane writes the group of its row -- the pivot lane to the
+// pivot-row buffer, the others to their own 16-B window of a scratch area
+// (wrow, chosen per step: row r's window for group J is scratch[2r + J], so
+// one instruction's windows are disjoint), so the store needs no exec switch
+// -- reads the pivot row's group back and takes a_j -= l * u_j.  The pivot
+// lane has l = 0: its row is unchanged up to the sign of zeros (sparse solves
+// only: every entry is finite there, so 0 * u is a zero).  A live group is
+// one SALU test and one branch besides its store, read and FMAs; the round-4
+// group (the pivot lane's store and the update of the rows below, each in its
+// own exec region) took four more SALU and one more branch.
+// (profiles/r5c_ab_lu_elig_groups.jsonl: config-2 launch -2.0 %, lone sample
+// -5 %; a variant whose pivot row also went through a window, its address
+// exchanged with 1/pivot, issued fewer instructions and ran 1 % slower,
+// profiles/r5h_ab_lu_windows.jsonl.)
+template <int I, int K, int CH>
+__device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32_t pmw, uint32_t gb, cf *wrow,
+                                              const LUBuf &L HC_LU_WORK_ARG) {
+    using C = LuChunks<CH>;
+    if constexpr (K < C::count(I)) {
+        constexpr int J = C::start(I, K), N = C::len(I, K);
+        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
+            if constexpr (N == 1) {
+                wrow[J] = rA[J];
+            } else {
+#pragma unroll
+                for (int q = 0; q < N; q += 2) st4(&wrow[J + q], rA[J + q], rA[J + q + 1]);
+            }
+            wave_lds_sync();
+            HC_LU_WORK(N);
+#ifdef HC_DIAG_LUWORK
+            lu_work_acc.groups++;
+#endif
+            cf u[N];
+            if constexpr (N == 1) {
+                u[0] = L.row[J];
+            } else {
+#pragma unroll
+                for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
+            }
+#pragma unroll
+            for (int q = 0; q < N; q++) {
+                const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, l, pf2{u[q].x, u[q].y});
+                rA[J + q] = cmk(v.x, v.y);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        lu_group_elig<I, K + 1, CH>(rA, l, pmw, gb, wrow, L HC_LU_WORK_PASS);
+    }
+}
+
 // The rest of pivot step I once the pivots are chosen: broadcast, relabel,
 // 1/pivot, update.  DENSE (the whole solve of a matrix that is not provably
 // finite or that met a pivot outside the fast reciprocal range): every column
@@ -306,7 +359,8 @@ __device__ __forceinline__ void lu_store_update(cf (&rA)[NV], const cf &l, uint3
 // reports such a solve, and the caller solves the system again densely.
 template <int I, bool DENSE, int CH>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
-                                             bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s, bool elig HC_LU_WORK_ARG) {
+                                             cf *scr, bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s,
+                                             bool elig HC_LU_WORK_ARG) {
     constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
     uint32_t pmw = FULL;
     if constexpr (!DENSE) {
@@ -359,7 +413,15 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // the update; the abort kernel (groups of 4, latency: its time to the first
     // pose) keeps the two loops, whose stores all issue before the first
     // update reads (profiles/r4q_ttfp_abort_structure.jsonl)
-    if constexpr (CH == 2) {
+    if constexpr (CH == 2 && !DENSE) {
+        // the eligible rows' region (round 5): the pivot lane writes the groups
+        // to the buffer, the rows below to their scratch windows
+        cf *wrow = is_piv ? L.row : scr;
+#ifdef HC_DIAG_LUWORK
+        lu_work_acc.excl = __builtin_amdgcn_ballot_w64(is_piv);
+#endif
+        if (elig) lu_group_elig<I, 0, CH>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
+    } else if constexpr (CH == 2) {
         lu_store_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
     } else if (below) {
         lu_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
@@ -371,7 +433,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
 // garbage, the caller discards it and solves densely).
 template <int I, bool DENSE, int CH>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
-                                           bool row_lane, PivF &my, LUBuf &L, bool &redo HC_LU_WORK_ARG) {
+                                           bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
         HC_ISA_MARK_I("lu_search", I);
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
@@ -452,8 +514,8 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl1 = 32 + __builtin_ctz(mhi);
         }
         HC_ISA_MARK_I("lu_pattern", I);
-        lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, is_piv, pl0, pl1, reg_s, oo_s, elig HC_LU_WORK_PASS);
-        lu_forward<I + 1, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo HC_LU_WORK_PASS);
+        lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, scr, is_piv, pl0, pl1, reg_s, oo_s, elig HC_LU_WORK_PASS);
+        lu_forward<I + 1, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scr, redo HC_LU_WORK_PASS);
     }
 }
 
@@ -505,9 +567,14 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 // not provably finite or a pivot outside the fast reciprocal range: the
 // caller then rebuilds the system and calls the DENSE solve, the reference
 // algorithm step for step (both exact).
+// scratch: this half's LU_SCRATCH_CF entries (16-B aligned) that the sparse
+// solve with groups of 2 may overwrite: the store windows of the eligible
+// rows (row r writes column group J at scratch[2r + J]); the caller's data
+// there is lost.
+constexpr int LU_SCRATCH_CF = 2 * (NV - 1) + NV;   // 88
 template <bool DENSE, int CH = LU_CHUNK>
-__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, bool &redo,
-                                      unsigned long long count_mask = ~0ull) {
+__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
+                                      bool &redo, unsigned long long count_mask = ~0ull) {
     (void)count_mask;   // diagnostic builds (HC_DIAG_LUWORK): lanes whose executed work is counted
     const int r = lane & 31, hb = lane & 32;
     const bool row_lane = r < NV;
@@ -537,8 +604,8 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     uint32_t pat = row_lane ? pattern : 0u;
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
-    LuWork lu_work_acc{0ull, count_mask, 0ull, 0ull};
-    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo, lu_work_acc);
+    LuWork lu_work_acc{0ull, count_mask, 0ull, 0ull, 0ull};
+    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
     if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
@@ -549,7 +616,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     }
     if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
-    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, redo);
+    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo);
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
     HC_ISA_MARK("lu_back_init");
