@@ -1275,16 +1275,19 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             // LU, act / pred would be spilled)
             HC_ISA_MARK("redo_evals");
             const bool act_r = S.st.ph == PH_STAGE, pred_r = act_r && S.st.s < 4;
+            // a fresh lane id: the table addresses of the stage's evaluations
+            // are not shared with (and held across the LU for) this rare path
+            const int r_r = lane_fresh() & 31;
             cf rb = cmk(0.0f, 0.0f);
             if (__ballot(pred_r) != 0ull) {
-                const cf t = eval_rhs<RHS_HT>(s_ht, S, r_v, true, rhs_masks(T));
+                const cf t = eval_rhs<RHS_HT>(s_ht, S, r_r, true, rhs_masks(T));
                 if (pred_r) rb = t;
             }
             if (__ballot(act_r && !pred_r) != 0ull) {
-                const cf t = eval_rhs<RHS_H>(s_ht, S, r_v, false, rhs_masks(T));
+                const cf t = eval_rhs<RHS_H>(s_ht, S, r_r, false, rhs_masks(T));
                 if (!pred_r) rb = t;
             }
-            eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_v);
+            eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_r);
             wave_lds_sync();
 #ifdef HC_DIAG_LUWORK
             k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, S.ent, redo, __ballot(act_r));
@@ -1862,9 +1865,10 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.8 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps and "
-           "readlane back substitution, pipelined evals over per-slot prefix tables, 5 waves/SIMD, time slicing "
-           "at step boundaries with least-attained-service issue priority)";
+    return "hc_trifocal gfx950 v9.9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+           "column groups in the eligible rows' exec region through scratch windows, readlane back substitution, "
+           "pipelined evals over per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with "
+           "least-attained-service issue priority)";
 }
 
 }  // extern "C"
