@@ -12,7 +12,7 @@ for b in ${BUILDS:-abe4 abc2}; do
   HC_TRIFOCAL_LIB=$P/libhc_trifocal_$b.so timeout -k 10 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread -k "abort or config3" > gpurun_out/${T}_parity_$b.log 2>&1; rc=$?; tail -1 gpurun_out/${T}_parity_$b.log; [ $rc -eq 0 ] || exit $rc
 done
 for r in 0 1 2; do
-  for b in p1 ${BUILDS:-abe4 abc2}; do
+  for b in ${BASE:-p1} ${BUILDS:-abe4 abc2}; do
     HC_TRIFOCAL_LIB=$P/libhc_trifocal_$b.so timeout -k 10 120 python scripts/ttfp.py 12 > gpurun_out/${T}_tmp.json || exit 1
     python -c "import json,sys; d=json.load(open('gpurun_out/${T}_tmp.json')); d.update(build='$b', round=$r); print(json.dumps(d))" >> gpurun_out/${T}_ttfp.jsonl
   done

@@ -844,7 +844,11 @@ __device__ unsigned long long g_diag_phase[13];
 typedef uint32_t T_hxd_t[HX_NSLOT / 2][32];
 template <bool ABORT, int MINW, bool GTAB, bool ARCH = false>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
-    constexpr int LUCH = ABORT ? 4 : LU_CHUNK;   // LU column group (hc_lu.hpp): latency (abort) vs throughput
+    // LU (hc_lu.hpp): the abort kernel's time to the first pose is a lone
+    // path's latency, so it runs the latency mode (no exec region for the pivot
+    // row; profiles/r5n_ttfp.jsonl: -2.4 %); the tracking kernels the throughput one
+    constexpr int LUCH = LU_CHUNK;
+    constexpr bool LULAT = ABORT;
     constexpr int TAB_BYTES =
         GTAB ? 16 : (int)(sizeof(uint2) * HT_TERMS * 32 + sizeof(uint32_t) * HX_SLOT_CAP * 32 + sizeof(T_hxd_t));
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
@@ -1261,9 +1265,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         // (a dense re-solve evaluates dH/dx again)
         static_assert(ENT_CAP >= LU_SCRATCH_CF && offsetof(SlotLDS, ent) % 16 == 0, "LU scratch in SlotLDS::ent");
 #ifdef HC_DIAG_LUWORK
-        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, S.ent, redo, __ballot(act));   // :188 / :224
+        cf k = lu_solve<false, LUCH, LULAT>(rA, rB, lane_v, row_pat, LB, S.ent, redo, __ballot(act));   // :188 / :224
 #else
-        cf k = lu_solve<false, LUCH>(rA, rB, lane_v, row_pat, LB, S.ent, redo);                  // :188 / :224
+        cf k = lu_solve<false, LUCH, LULAT>(rA, rB, lane_v, row_pat, LB, S.ent, redo);                  // :188 / :224
 #endif
         HC_ISA_MARK("ctl_redo");
         if (__builtin_expect(redo, 0)) {
@@ -1865,10 +1869,11 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v9.9 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
-           "column groups in the eligible rows' exec region through scratch windows, readlane back substitution, "
-           "pipelined evals over per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with "
-           "least-attained-service issue priority)";
+    return "hc_trifocal gfx950 v10.0 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+           "one exec region per pivot step for the eligible rows with the column groups through scratch windows "
+           "(abort kernel: latency mode without exec regions), readlane back substitution, pipelined evals over "
+           "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
+           "issue priority)";
 }
 
 }  // extern "C"

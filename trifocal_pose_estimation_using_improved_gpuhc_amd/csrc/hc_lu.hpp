@@ -23,10 +23,14 @@
 //    it keeps the factors (o1, o2) for the back substitution;
 //  * broadcast: the pivot lane writes 1/pivot (in the pivot element's slot),
 //    rhs and rowid into its half's LDS buffer, every lane reads them back;
-//  * rows below the pivot: multiplier, right-hand side and fill-in pattern;
-//  * per column group (one uniform test): the pivot lane writes the group of
-//    its row (ds_write_b128), the rows below read it back (broadcast
-//    ds_read_b128) and update, 2 v_pk_fma_f32 per element.
+//  * one exec region of the eligible rows (the rows below and the pivot row,
+//    whose multiplier is zero; round 5): multiplier, right-hand side and
+//    fill-in pattern, then per column group (one uniform test) every eligible
+//    lane writes the group of its row (ds_write_b128; the pivot lane to the
+//    buffer, the others to their own scratch window) and reads the pivot
+//    row's group back (broadcast ds_read_b128) and updates, 2 v_pk_fma_f32 per
+//    element.  The abort kernel's latency mode also writes the pivot row's
+//    1/pivot, rhs and rowid from every lane (no exec region at all).
 //
 // Structural sparsity.  The trifocal Jacobian is sparse (170 of 900 entries
 // carry terms) and partial-pivot elimination fills it in only partly: on
@@ -49,8 +53,9 @@
 // the reference algorithm step for step.  So the sparse steps carry no dense
 // tests at all (a per-step `dense` flag cost ~12 SALU and 3 branches a step).
 //
-// The buffer is the path slot's SlotLDS::lu; the dH/dx entry block (SlotLDS::ent)
-// survives the solve, so a dense re-solve re-gathers the Jacobian from it.
+// The buffer is the path slot's SlotLDS::lu; the scratch windows are the dH/dx
+// entry block (SlotLDS::ent), dead once gathered into the registers (a dense
+// re-solve evaluates dH/dx again).
 #pragma once
 
 #include "hc_eval.hpp"
@@ -65,11 +70,13 @@ struct alignas(16) LUBuf {
 static_assert(sizeof(LUBuf) == sizeof(SlotLDS::lu), "LUBuf is SlotLDS::lu");
 static_assert(offsetof(SlotLDS, lu) % 16 == 0, "SlotLDS::lu must be 16-B aligned");
 
-// columns per skippable group (a template parameter CH below): 2 for the
-// tracking kernels, where the LDS stores of dead columns are what a wider group
-// costs (profiles/r3u_ab_oo_rz_gs_chunk2.jsonl: 33.55 -> 31.78 ms per config-2
-// launch), 4 for the abort kernel, whose time to the first pose is set by a
-// lone wave's latency (one group test per 4 columns; lone sample 11.2 vs 12.3 ms)
+// columns per skippable group (the template parameter CH below): 2, where the
+// LDS stores of dead columns are what a wider group costs
+// (profiles/r3u_ab_oo_rz_gs_chunk2.jsonl: 33.55 -> 31.78 ms per config-2
+// launch).  The abort kernel used groups of 4 in two loops until round 5, for
+// its lone-wave latency; groups of 2 in the eligible rows' region are as fast
+// there, and its latency mode faster (profiles/r5j_ttfp_abort_lu_variants.jsonl,
+// r5n_ttfp.jsonl)
 constexpr int LU_CHUNK = 2;
 
 // Correctly rounded 1/s for s in [2^-90, 2^120): v_rcp_f32 plus one Newton
@@ -185,25 +192,6 @@ __device__ __forceinline__ bool group_live(uint32_t pmw, uint32_t gb) {
     else return (gb >> J) & 1u;
 }
 
-// pivot lane: row elements of the groups of step I that are non-zero in some
-// pivot row of the wave
-template <int I, int K, int CH>
-__device__ __forceinline__ void lu_put_row(const cf (&rA)[NV], uint32_t pmw, uint32_t gb, LUBuf &L) {
-    using C = LuChunks<CH>;
-    if constexpr (K < C::count(I)) {
-        constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
-            if constexpr (N == 1) {
-                L.row[J] = rA[J];
-            } else {
-#pragma unroll
-                for (int q = 0; q < N; q += 2) st4(&L.row[J + q], rA[J + q], rA[J + q + 1]);
-            }
-        }
-        lu_put_row<I, K + 1, CH>(rA, pmw, gb, L);
-    }
-}
-
 #ifdef HC_DIAG_LUWORK
 // diagnostic build: rank-1 update elements the solves execute (sum over the
 // executed column groups of columns x active lanes), and the solves
@@ -224,37 +212,6 @@ struct LuWork { unsigned long long acc, mask, groups, rare, excl; };   // mask: 
 #define HC_LU_WORK_ARG
 #define HC_LU_WORK_PASS
 #endif
-
-// a_j -= l * u_j for the groups K.. of step I (the caller is inside the
-// below-the-pivot exec region)
-template <int I, int K, int CH>
-__device__ __forceinline__ void lu_update(cf (&rA)[NV], const cf &l, uint32_t pmw, uint32_t gb,
-                                          const LUBuf &L HC_LU_WORK_ARG) {
-    using C = LuChunks<CH>;
-    if constexpr (K < C::count(I)) {
-        constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
-            HC_LU_WORK(N);
-#ifdef HC_DIAG_LUWORK
-            lu_work_acc.groups++;
-#endif
-            cf u[N];
-            if constexpr (N == 1) {
-                u[0] = L.row[J];
-            } else {
-#pragma unroll
-                for (int q = 0; q < N; q += 2) ld4(&L.row[J + q], u[q], u[q + 1]);
-            }
-#pragma unroll
-            for (int q = 0; q < N; q++) {
-                const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, pf2{l.x, l.y}, pf2{u[q].x, u[q].y});
-                rA[J + q] = cmk(v.x, v.y);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        lu_update<I, K + 1, CH>(rA, l, pmw, gb, L HC_LU_WORK_PASS);
-    }
-}
 
 // the column groups K.. of step I: one uniform test per group (round 4; the
 // pivot row's stores and the update each tested every group before: 2.2 %
@@ -357,7 +314,7 @@ __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32
 // finite or that met a pivot outside the fast reciprocal range): every column
 // group and the IEEE reciprocal.  The sparse solve carries no dense tests: it
 // reports such a solve, and the caller solves the system again densely.
-template <int I, bool DENSE, int CH>
+template <int I, bool DENSE, int CH, bool LAT>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
                                              cf *scr, bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s,
                                              bool elig HC_LU_WORK_ARG) {
@@ -371,9 +328,18 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     }
     const uint32_t gb = group_bits<CH>(pmw);
     HC_ISA_MARK_I("lu_store", I);
-    if (is_piv) {                                          // pivot row -> buffer, 1/pivot in the pivot's slot
+    // latency mode (LAT, the abort kernel): every lane writes, the pivot lane to
+    // the buffer, the others to their scratch windows -- no exec region, at the
+    // price of LDS bandwidth (profiles/r5m_ab_lu_x.jsonl: lone sample -2 %,
+    // loaded launch +0.8 %)
+    constexpr bool X1 = LAT && CH == 2 && !DENSE;
+    cf *wrow = nullptr;
+    if constexpr (X1) {
+        wrow = is_piv ? L.row : scr;
+        wrow[I] = cmk(reg_s.x, reg_s.y);
+        st4(&wrow[30], rB, cmk(__int_as_float(rowid), 0.0f));
+    } else if (is_piv) {                                   // pivot row -> buffer, 1/pivot in the pivot's slot
         L.row[I] = cmk(reg_s.x, reg_s.y);
-        if constexpr (CH != 2) lu_put_row<I, 0, CH>(rA, pmw, gb, L);
         L.row[30] = rB;
         L.row[31].x = __int_as_float(rowid);
     }
@@ -383,10 +349,16 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     cf sB0, pr;
     ld4(&L.row[30], sB0, pr);
     const int piv_pos = __float_as_int(pr.x);
-    if (is_piv) rowid = I;                                 // :70-82
-    else if (rowid == I) rowid = piv_pos;
-    // the pivot lane keeps its factors (computed in the search, lu_forward)
-    if (is_piv) my.oo = oo_s;
+    if constexpr (X1) {
+        rowid = is_piv ? I : (rowid == I ? piv_pos : rowid);   // :70-82
+        my.oo.x = is_piv ? oo_s.x : my.oo.x;
+        my.oo.y = is_piv ? oo_s.y : my.oo.y;
+    } else {
+        if (is_piv) rowid = I;                                 // :70-82
+        else if (rowid == I) rowid = piv_pos;
+        // the pivot lane keeps its factors (computed in the search, lu_forward)
+        if (is_piv) my.oo = oo_s;
+    }
     // opaque: the select chain must be resolved here, not carried as 30
     // per-step factor pairs into the back substitution
     asm volatile("" : "+v"(my.oo));
@@ -399,6 +371,27 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // fill-in pattern (branch-free) and the rank-1 update.  Fill-in: a row
     // below whose column I may be non-zero takes the pivot patterns (both
     // halves': a superset of its own pivot row's).
+    if constexpr (CH == 2 && !DENSE) {
+        // the multiplier, right-hand side and fill-in pattern in the eligible
+        // rows' region too (the pivot lane's multiplier is zeroed: its rhs and
+        // row stay, up to the sign of zeros), one exec region per step
+        // (profiles/r5m_ab_lu_x.jsonl: -0.4 %, lone sample -1.5 %)
+        HC_ISA_MARK_I("lu_update", I);
+        if constexpr (!X1) wrow = is_piv ? L.row : scr;
+#ifdef HC_DIAG_LUWORK
+        lu_work_acc.excl = __builtin_amdgcn_ballot_w64(is_piv);
+#endif
+        if (elig) {
+            HC_ISA_MARK_I("lu_mult", I);
+            pf2 lq = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+            const pf2 lp = {is_piv ? 0.0f : lq.x, is_piv ? 0.0f : lq.y};
+            const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
+            rB = cmk(bp.x, bp.y);
+            pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
+            lu_group_elig<I, 0, CH>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
+        }
+        return;
+    }
     pf2 lp = {0.0f, 0.0f};
     if (below) {
         HC_ISA_MARK_I("lu_mult", I);
@@ -409,29 +402,16 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         if constexpr (!DENSE) pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
     }
     HC_ISA_MARK_I("lu_update", I);
-    // the tracking kernels (groups of 2) test each group once for the store and
-    // the update; the abort kernel (groups of 4, latency: its time to the first
-    // pose) keeps the two loops, whose stores all issue before the first
-    // update reads (profiles/r4q_ttfp_abort_structure.jsonl)
-    if constexpr (CH == 2 && !DENSE) {
-        // the eligible rows' region (round 5): the pivot lane writes the groups
-        // to the buffer, the rows below to their scratch windows
-        cf *wrow = is_piv ? L.row : scr;
-#ifdef HC_DIAG_LUWORK
-        lu_work_acc.excl = __builtin_amdgcn_ballot_w64(is_piv);
-#endif
-        if (elig) lu_group_elig<I, 0, CH>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
-    } else if constexpr (CH == 2) {
-        lu_store_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
-    } else if (below) {
-        lu_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L HC_LU_WORK_PASS);
-    }
+    // the dense re-solve: one test per group for the pivot lane's store and the
+    // update of the rows below (round 4; the dense steps may hold inf and NaN,
+    // so the pivot row cannot take a zero multiplier there)
+    lu_store_update<I, 0, CH>(rA, cmk(lp.x, lp.y), pmw, gb, L, is_piv, below HC_LU_WORK_PASS);
 }
 
 // One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
 // outside the fast reciprocal range sets `redo` (the solve goes on with
 // garbage, the caller discards it and solves densely).
-template <int I, bool DENSE, int CH>
+template <int I, bool DENSE, int CH, bool LAT>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
                                            bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
@@ -514,8 +494,9 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl1 = 32 + __builtin_ctz(mhi);
         }
         HC_ISA_MARK_I("lu_pattern", I);
-        lu_step_body<I, DENSE, CH>(rA, rB, rowid, pat, my, L, scr, is_piv, pl0, pl1, reg_s, oo_s, elig HC_LU_WORK_PASS);
-        lu_forward<I + 1, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scr, redo HC_LU_WORK_PASS);
+        lu_step_body<I, DENSE, CH, LAT>(rA, rB, rowid, pat, my, L, scr, is_piv, pl0, pl1, reg_s, oo_s,
+                                        elig HC_LU_WORK_PASS);
+        lu_forward<I + 1, DENSE, CH, LAT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scr, redo HC_LU_WORK_PASS);
     }
 }
 
@@ -571,10 +552,14 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 // solve with groups of 2 may overwrite: the store windows of the eligible
 // rows (row r writes column group J at scratch[2r + J]); the caller's data
 // there is lost.
-constexpr int LU_SCRATCH_CF = 2 * (NV - 1) + NV;   // 88
-template <bool DENSE, int CH = LU_CHUNK>
+constexpr int LU_SCRATCH_CF = 2 * 31 + 32;   // 94: lane r's window scratch[2r .. 2r + 31]
+template <bool DENSE, int CH = LU_CHUNK, bool LAT = false>
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
-                                      bool &redo, unsigned long long count_mask = ~0ull) {
+                                      bool &redo, unsigned long long count_mask = ~0ull);
+template <bool DENSE, int CH, bool LAT>
+__device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
+                                      bool &redo, unsigned long long count_mask) {
+    static_assert(CH == 2, "column groups of 2 (the scratch windows are 16 B)");
     (void)count_mask;   // diagnostic builds (HC_DIAG_LUWORK): lanes whose executed work is counted
     const int r = lane & 31, hb = lane & 32;
     const bool row_lane = r < NV;
@@ -605,7 +590,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
     LuWork lu_work_acc{0ull, count_mask, 0ull, 0ull, 0ull};
-    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, lu_work_acc);
+    lu_forward<0, DENSE, CH, LAT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
     if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
@@ -616,7 +601,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     }
     if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
-    lu_forward<0, DENSE, CH>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo);
+    lu_forward<0, DENSE, CH, LAT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo);
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
     HC_ISA_MARK("lu_back_init");
