@@ -1291,7 +1291,11 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                 const cf t = eval_rhs<RHS_H>(s_ht, S, r_r, false, rhs_masks(T));
                 if (!pred_r) rb = t;
             }
-            eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_r);
+            // (eval_hx without its phase marker: the ISA phase count keeps this rare
+            // copy under redo_evals)
+            eval_hx_terms(s_hx, s_hxd, reinterpret_cast<char *>(&S), r_r);
+            wave_lds_sync();
+            gather_hx(rA, &s_rowc[0][0], S, r_r);
             wave_lds_sync();
 #ifdef HC_DIAG_LUWORK
             k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, S.ent, redo, __ballot(act_r));
