@@ -1607,12 +1607,14 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
                 k.rq ? (unsigned)susp_end : 0u};
     hipLaunchKernelGGL(k_prep_tables, dim3(1), dim3(PREP_THREADS), 0, s, pa);
     if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-    // tracking: term tables read from the workspace (L1/L2), 96 VGPRs, 27.6 KB LDS
-    // per workgroup -> 5 waves/SIMD.  Abort mode keeps the tables in LDS at 4
-    // waves/SIMD (the scoring path needs the registers).
+    // term tables read from the workspace (L1/L2).  Tracking: 96 VGPRs, 31 KB
+    // LDS per workgroup -> 5 waves/SIMD.  Abort mode: 4 waves/SIMD (the scoring
+    // path needs the registers); its tables moved out of the LDS in round 5,
+    // where the other waves' LDS traffic was delaying the earliest hypotheses
+    // (time to the first pose -2.8 %, profiles/r5q_ttfp_probe.jsonl)
     const bool archived = !truncate || explicit_rk;
     if (abort_mode && archived) return HC_ERROR_INVALID_VALUE;
-    const void *kern = abort_mode ? (const void *)k_track<true, 4, false>
+    const void *kern = abort_mode ? (const void *)k_track<true, 4, true>
                        : archived ? (const void *)k_track<false, 5, true, true>
                                   : (const void *)k_track<false, 5, true>;
     const int grid = grid_for((int)((paths + 1) / 2), kern);
