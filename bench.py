@@ -170,6 +170,21 @@ def spawn_ranks(gpus, argv):
         return 1
 
 
+def rank_abort_record(g, runs, shard_paths, chunk_paths):
+    """One rank's abort-leg record from its runs' (found itself, paths tracked,
+    found byte) triples.  A rank that found nothing itself and tracked fewer
+    paths than its shard was stopped by another rank's find; inside a launch
+    when the count is not a whole number of chunks (the chunk-boundary
+    reduction stops a rank only between chunks, the device flag inside one)."""
+    tr = [int(x[1]) for x in runs]
+    pstop = [not x[0] and int(x[1]) < shard_paths for x in runs]
+    mid = [p and int(x[1]) % chunk_paths != 0 for p, x in zip(pstop, runs)]
+    return {"rank": g, "shard_paths": shard_paths,
+            "self_found_runs": int(sum(1 for x in runs if x[0])),
+            "paths_tracked": {"median": int(np.median(tr)), "min": min(tr), "max": max(tr)},
+            "peer_stopped_runs": int(sum(pstop)), "peer_stopped_mid_launch_runs": int(sum(mid))}
+
+
 def gather_floats(vals, dev, world):
     """Every rank's list of floats (same length on every rank), rank-ordered."""
     if world == 1:
@@ -418,20 +433,8 @@ def main():
                                 "min": round(float(np.min(v)) * 1e3, 3), "max": round(float(np.max(v)) * 1e3, 3)}
             shards = [sharding.shard(Sa * world, world, g)[1] * 312 for g in range(world)]
             chunk_paths = args.abort_chunk * 312
-            ranks = []
-            for g in range(world):
-                runs = [pr[g] for pr in per_rank_runs]
-                tr_g = [int(x[1]) for x in runs]
-                # a rank that found nothing itself and tracked fewer paths than its
-                # shard was stopped by another rank's find; mid-launch when the count
-                # is not a whole number of chunks (the chunk-boundary reduction
-                # stops only between chunks, the device flag inside a launch)
-                pstop = [not x[0] and int(x[1]) < shards[g] for x in runs]
-                mid = [p and int(x[1]) % chunk_paths != 0 for p, x in zip(pstop, runs)]
-                ranks.append({"rank": g, "shard_paths": shards[g],
-                              "self_found_runs": int(sum(1 for x in runs if x[0])),
-                              "paths_tracked": {"median": int(np.median(tr_g)), "min": min(tr_g), "max": max(tr_g)},
-                              "peer_stopped_runs": int(sum(pstop)), "peer_stopped_mid_launch_runs": int(sum(mid))})
+            ranks = [rank_abort_record(g, [pr[g] for pr in per_rank_runs], shards[g], chunk_paths)
+                     for g in range(world)]
             abort_info[key] = {
                 "found": all(found_runs),
                 "found_runs": int(sum(found_runs)),

@@ -47,6 +47,19 @@ def test_bench_line_fields_from_helpers():
     assert 15.5e6 < b < 16.5e6 and abs(b / 31200 - 512) < 10
 
 
+def test_rank_abort_record_classifies_peer_stops():
+    chunk = 125 * 312
+    shard = 1000 * 312
+    runs = [(1.0, 14000.0, 1.0),          # found itself
+            (0.0, 2 * chunk, 1.0),        # stopped between chunks (a whole number of them)
+            (0.0, chunk + 777, 1.0),      # stopped inside a launch by the device flag
+            (0.0, float(shard), 1.0)]     # tracked its whole shard: not stopped
+    r = bench.rank_abort_record(3, runs, shard, chunk)
+    assert r["rank"] == 3 and r["self_found_runs"] == 1
+    assert r["peer_stopped_runs"] == 2 and r["peer_stopped_mid_launch_runs"] == 1
+    assert r["paths_tracked"] == {"median": int((2 * chunk + chunk + 777) / 2), "min": 14000, "max": shard}
+
+
 @pytest.mark.timeout(300)
 def test_bare_multi_gpu_run_without_gpus_fails_loudly(tmp_path):
     """No GPU here: the bare --gpus 2 run starts two ranks, both fail at
