@@ -45,7 +45,12 @@ def main():
     if "--sigma" in argv:   # noisy synthcurves of the dataset (trifocal_..._amd/synthcurves.py)
         from trifocal_pose_estimation_using_improved_gpuhc_amd import synthcurves
         data = synthcurves.noisy(data, float(argv[argv.index("--sigma") + 1]), synthcurves.DEFAULT_SEED)
-    tgt, dif, _ = prepare_target_params(problem, data, seed, 100)
+    if "--shard8" in argv:   # rank g's shard of an 8-GPU config-2 run
+        g8 = int(argv[argv.index("--shard8") + 1])
+        ta, da, _ = prepare_target_params(problem, data, seed, 800, num_gpus=8)
+        tgt, dif = ta[100 * g8:100 * g8 + 100].copy(), da[100 * g8:100 * g8 + 100].copy()
+    else:
+        tgt, dif, _ = prepare_target_params(problem, data, seed, 100)
     scaled = "--scaled" in argv
     if scaled:
         tgt = np.stack([tgt[0]] + [(tgt[0] * np.float32(s)).astype(np.float32) for s in (2.0 ** 40, 2.0 ** 70)])
