@@ -9,7 +9,7 @@ the pivot-pattern readlanes, the pivot-row stores, the read-back + 1/pivot +
 relabelling, the multiplier and right-hand side, the column-group updates and
 the back-substitution step.  Inside the LU the column-group bodies (a
 `s_bitcmp` + `s_cbranch_scc1` skip over a store or an update of one group)
-are counted apart from the unconditional instructions, so that
+(or a two-column `s_and_b32` + `s_cmp_eq_u32` test) are counted apart from the unconditional instructions, so that
 scripts/phase_breakdown.py can weigh them with the dynamic frequencies the
 HC_DIAG_LUWORK build measures (live groups, rare steps and evaluation kinds
 per wave-stage) and check the sum against the rocprofv3 PMC totals.
@@ -57,6 +57,11 @@ def compile_asm(path):
     subprocess.run(cmd, check=True, capture_output=True)
 
 
+# scalar instructions that leave SCC alone (between a group test and its branch)
+SCC_KEEP = ("s_mov_b32", "s_mov_b64", "s_waitcnt", "s_setprio", "s_cbranch_execz", "s_cbranch_execnz",
+            "s_cbranch_vccz", "s_cbranch_vccnz")
+
+
 def kernel_lines(asm):
     lines = open(asm).read().splitlines()
     start = next(i for i, ln in enumerate(lines) if ln.startswith(KERNEL + ":"))
@@ -102,15 +107,17 @@ def analyse(lines):
             body[1][cls] += 1
         else:
             ph["fixed"][cls] += 1
-        if mn.startswith("s_bitcmp"):
+        # the group test: the last SCC write before the s_cbranch_scc1 is a bit
+        # test (s_bitcmp0 of one column's bit) or a two-column test (s_and_b32 of
+        # the pair's bits + s_cmp_eq_u32 with 0); the scheduler may put VALU or
+        # LDS work between the test and its branch
+        if mn.startswith("s_bitcmp") or (mn == "s_cmp_eq_u32" and t.rstrip().endswith(", 0")):
             prev_bitcmp = True
             continue
         if prev_bitcmp and mn == "s_cbranch_scc1" and skip_to is None and "lu_" in cur:
             skip_to = t.split()[1]
             body = (cur, collections.Counter())
-        if mn != "s_cbranch_scc1" and not mn.startswith("ds_write") and not mn.startswith("s_nop"):
-            prev_bitcmp = False
-        elif mn == "s_cbranch_scc1":
+        if mn == "s_cbranch_scc1" or (mn.startswith("s_") and mn not in SCC_KEEP and not mn.startswith("s_nop")):
             prev_bitcmp = False
     return phases
 

@@ -81,7 +81,11 @@ def main():
     rl_common = min(rare_fixed["valu_readlane"], 2 * 28)
     rare_fixed["valu_readlane"] -= rl_common
     st_body, _ = bodies("lu_store")
-    up_body, _ = bodies("lu_update")
+    # the update's column-group bodies: under the lu_update marker up to round 4;
+    # from round 5 (one exec region per pivot step) they follow the lu_mult marker
+    up_body, n_up = bodies("lu_update")
+    mu_body, n_mu = bodies("lu_mult")
+    up_body = {c: (up_body[c] * n_up + mu_body[c] * n_mu) / max(1, n_up + n_mu) for c in CLASSES}
     rows = {
         "lu_search": sc(fixed("lu_search"), solves),
         "lu_rare_path": sc(rare_fixed, solves * rare / 30.0),
