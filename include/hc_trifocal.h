@@ -206,7 +206,11 @@ hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspa
                         8, 5, 3, 3, 1, 1 terms (or a row of more than 6
                         entries), or a dH/dt | H row of more than 13 terms
                         whose partner row (lane ^ 16) has more than 10
-                        (Evaluations);
+                        (Evaluations); tracker launches also
+                        when a row's dH/dx structure has an entry outside
+                        trifocal_2op1p_30x30's (the LU skips the column
+                        groups that structure can never fill; the
+                        evaluation entry points take any structure);
      HC_ERROR_DEVICE -- time slicing only: a suspended path could not be handed
                         over (the ring overflowed: more than 4096 re-pushes of
                         abandoned tickets in one launch; or a ring entry

@@ -18,6 +18,14 @@ extern "C" {
 #define HC_RING_TEST_MIN_TICKS 4096
 void hc_trifocal_set_ring_test(int delay_ticks);
 
+/* The tracker LU's compiled-in structure (hc_lu.hpp): row `row`'s structural
+   pattern of trifocal_2op1p_30x30's dH/dx (bit c: entry (row, c) has terms),
+   and the class of column group `group` of pivot step `step` (groups of 2
+   after a leading single column when step + 1 is odd): 0 tested, 1 dead (the
+   symbolic fill-in bound excludes it), 2 always run; -1 out of range. */
+unsigned hc_lu_struct_pattern(int row);
+int hc_lu_group_class(int step, int group);
+
 #ifdef __cplusplus
 }
 #endif

@@ -553,3 +553,33 @@ def test_eval_rejects_tables_without_helpers(problem):
     torch.cuda.synchronize(dev)
     assert int(L.hc_trifocal_workspace_status(p(ws))) == 5   # HC_ERROR_TABLE
     assert (HX == 7.0).all() and (HT == 7.0).all() and (H == 7.0).all()
+
+
+def test_tracker_rejects_structure_outside_its_lu(problem, samples100, tracker):
+    """A row-permuted system (valid and equivalent) has a dH/dx structure
+    outside the one the tracker's LU compiles in (hc_lu.hpp LU_STRUCT_PAT:
+    the column groups it never tests): the evaluation entry points take it
+    (test_eval_row_permuted_tables_match_oracle), the tracker refuses it with
+    HC_ERROR_TABLE and leaves its outputs untouched, and the problem's own
+    tables still track afterwards."""
+    import dataclasses
+    import torch
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+    from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker
+    perm = np.arange(30)
+    perm[0], perm[9] = 9, 0
+    dx, dt, _ = _row_permuted(problem, perm)
+    dev = torch.device("cuda:0")
+    tr = DeviceTracker(dataclasses.replace(problem, dHdx_index=dx, dHdt_index=dt), dev)
+    tgt, dif, _ = samples100
+    r = tr.allocate(1)
+    tr.reset_tracks(r)
+    r.converge.fill_(7)
+    tr.launch(torch.from_numpy(tgt[:1]).to(dev), torch.from_numpy(dif[:1]).to(dev), r)
+    torch.cuda.synchronize(dev)
+    assert int(tr.L.hc_trifocal_workspace_status(ctypes.c_void_p(tr.workspace.data_ptr()))) == 5   # HC_ERROR_TABLE
+    with pytest.raises(_abi.HCError):
+        tr.workspace_status()
+    assert (r.converge == 7).all()
+    ok = tracker.track(tgt[:1], dif[:1]).host()
+    assert ok["converge"].sum() > 0

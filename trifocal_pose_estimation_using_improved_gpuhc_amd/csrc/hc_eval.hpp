@@ -105,7 +105,7 @@ struct EvalTables {
     int hx_len;
     int status;
     unsigned magic;                   // TAB_MAGIC once built: the tables persist in the workspace
-    unsigned pad;
+    unsigned lu_struct;               // 1: the dH/dx structure lies within the tracker LU's (hc_lu.hpp LU_STRUCT_PAT)
     unsigned long long src_hash;      // hash of the unified index they were built from
     unsigned long long pad2;
     uint32_t gm[GM_WORDS][32];

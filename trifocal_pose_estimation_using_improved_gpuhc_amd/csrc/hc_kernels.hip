@@ -358,6 +358,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
     EvalTables *T = &ws->tab;
     __shared__ int s_len[32];
     __shared__ int s_bad;
+    __shared__ int s_nostruct;   // the dH/dx structure is not within the tracker LU's
     __shared__ unsigned long long s_h[PREP_THREADS];
     __shared__ unsigned s_cleared, s_dlo, s_dhi;
     __shared__ int s_valid;
@@ -374,6 +375,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         unsigned *cb = reinterpret_cast<unsigned *>(ws);
         for (int q = 0; q < 16; q++) cb[q] = 0u;
         s_bad = 0;
+        s_nostruct = 0;
         if (pa.found_in) {
             const bool peer = pa.peer_found &&
                               __hip_atomic_load(pa.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u;
@@ -597,6 +599,10 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
             T->gm[q][r] = v;
         }
         T->pat[r] = pat;
+        // the tracker's LU skips the column groups this problem's structure
+        // can never fill (hc_lu.hpp LU_STRUCT_PAT); the evaluations take any
+        // structure, the tracker only one within it
+        if (r < NV && (pat & ~LU_STRUCT_PAT[r]) != 0u) atomicOr(&s_nostruct, 1);
         for (int q = 0; q < HX_NSLOT / 2; q++) T->hxd[q][r] = s_dst[q][r];
         if (r < NV)
             for (int c = 0; c < NV; c++) {
@@ -761,6 +767,7 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
         for (int q = 0; q < 32; q++) mx = max(mx, s_len[q]);
         T->hx_len = mx;
         T->status = s_bad ? HC_ERROR_TABLE : 0;
+        T->lu_struct = s_nostruct ? 0u : 1u;
         T->src_hash = src_hash;
         T->magic = TAB_MAGIC;
         if (s_bad) ws->status = HC_ERROR_TABLE;
@@ -849,6 +856,12 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     // row; profiles/r5n_ttfp.jsonl: -2.4 %); the tracking kernels the throughput one
     constexpr int LUCH = LU_CHUNK;
     constexpr bool LULAT = ABORT;
+    // the column-group classes of this problem's structure (hc_lu.hpp; the
+    // tables' check guarantees the loaded structure lies within it)
+#ifndef HC_LU_STRUCT
+#define HC_LU_STRUCT 1
+#endif
+    constexpr bool LUSTRUCT = HC_LU_STRUCT != 0;
     constexpr int TAB_BYTES =
         GTAB ? 16 : (int)(sizeof(uint2) * HT_TERMS * 32 + sizeof(uint32_t) * HX_SLOT_CAP * 32 + sizeof(T_hxd_t));
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
@@ -857,6 +870,10 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     Workspace *ws = a.ws;
     const EvalTables *T = &ws->tab;
     if (ws->status != 0u) return;
+    if (LUSTRUCT && T->lu_struct != 1u) {   // a structure the tracker's LU does not cover
+        if (threadIdx.x == 0) atomicMax(&ws->status, (unsigned)HC_ERROR_TABLE);
+        return;
+    }
     // time slicing: this launch's ring epoch (bumped by k_prep_tables)
     const unsigned epoch = (!ABORT && a.slice_q > 0) ? ld_rlx(&a.rq[RQ_EPOCH]) : 0u;
     const uint2 *s_ht = GTAB ? T->ht : reinterpret_cast<const uint2 *>(s_tab);
@@ -1265,9 +1282,9 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
         // (a dense re-solve evaluates dH/dx again)
         static_assert(ENT_CAP >= LU_SCRATCH_CF && offsetof(SlotLDS, ent) % 16 == 0, "LU scratch in SlotLDS::ent");
 #ifdef HC_DIAG_LUWORK
-        cf k = lu_solve<false, LUCH, LULAT>(rA, rB, lane_v, row_pat, LB, S.ent, redo, __ballot(act));   // :188 / :224
+        cf k = lu_solve<false, LUCH, LULAT, LUSTRUCT>(rA, rB, lane_v, row_pat, LB, S.ent, redo, __ballot(act));   // :188 / :224
 #else
-        cf k = lu_solve<false, LUCH, LULAT>(rA, rB, lane_v, row_pat, LB, S.ent, redo);                  // :188 / :224
+        cf k = lu_solve<false, LUCH, LULAT, LUSTRUCT>(rA, rB, lane_v, row_pat, LB, S.ent, redo);                  // :188 / :224
 #endif
         HC_ISA_MARK("ctl_redo");
         if (__builtin_expect(redo, 0)) {
@@ -1680,6 +1697,18 @@ int hc_diag_luwork(unsigned long long *out, int reset) {
 }
 #endif
 
+#ifdef HC_DIAG_LIVE
+int hc_diag_live(unsigned long long *out, int reset) {
+    constexpr size_t n = sizeof(unsigned long long) * hc::NV * (hc::LIVE_SOLVES + 1);
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(hc::g_diag_live), n) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long z[hc::NV * (hc::LIVE_SOLVES + 1)] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(hc::g_diag_live), z, n) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
 size_t hc_trifocal_workspace_size(void) { return hc::ws_bytes_needed(); }
 
 size_t hc_trifocal_workspace_size_for(int sub_ransac_iters) {
@@ -1868,6 +1897,14 @@ int hc_diag_util(unsigned long long *out, int reset) {
 
 int hc_trifocal_abi_version(void) { return HC_TRIFOCAL_ABI_VERSION; }
 
+// tests only (include/hc_trifocal_testing.h): the tracker LU's structural
+// patterns and column-group classes (hc_lu.hpp)
+unsigned hc_lu_struct_pattern(int row) { return row >= 0 && row < hc::NV ? hc::LU_STRUCT_PAT[row] : 0u; }
+int hc_lu_group_class(int step, int group) {
+    if (step < 0 || step >= hc::NV - 1 || group < 0 || group >= hc::LuChunks<2>::count(step)) return -1;
+    return hc::lu_group_class<2>(step, group);
+}
+
 void hc_trifocal_set_ring_test(int delay_ticks) {
     hc::g_ring_test.store(delay_ticks > 0 ? (delay_ticks < HC_RING_TEST_MIN_TICKS ? HC_RING_TEST_MIN_TICKS : delay_ticks)
                                           : 0,
@@ -1875,8 +1912,9 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.0 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
-           "one exec region per pivot step for the eligible rows with the column groups through scratch windows "
+    return "hc_trifocal gfx950 v10.1 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+           "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
+           "column groups by structural class (never-fillable groups untested, always-live groups unconditional) "
            "(abort kernel: latency mode without exec regions), readlane back substitution, pipelined evals over "
            "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
            "issue priority)";

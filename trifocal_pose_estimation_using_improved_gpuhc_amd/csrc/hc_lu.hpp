@@ -174,6 +174,64 @@ struct LuChunks {
     static constexpr uint32_t mask(int I, int k) { return ((1u << len(I, k)) - 1u) << start(I, k); }
 };
 
+// The tracker's column groups by class (round 5).  The sparse LU tests a
+// group live when a pivot row of the wave may be non-zero there; for this
+// problem's Jacobian most outcomes are fixed in advance:
+//  * dead: the symbolic fill-in bound -- at step I every row pattern is within
+//    the row's bound cur[r], the pivot rows' within S_I = OR of the bounds of
+//    the rows that may hold column I, and a row that may hold column I grows
+//    by at most S_I -- has no column of the group: the test can never pass
+//    (101 of the 225 groups of a solve);
+//  * always: live in every one of the 1.2 M sampled wave-solves of datasets
+//    000/001/002 (profiles/r5lv_live.jsonl; 16 of the 40 provably, from the
+//    rows that must hold column I): no test, the update runs.  Running a group
+//    that happens to be dead is exact: the pivot rows hold zeros there, and a
+//    - l * 0 == a (up to the sign of a zero; l is finite in the sparse solve);
+//  * tested: the other 84.
+// Only the tracker's solves (STRUCT) use the classes: k_tables checks that the
+// loaded problem's structural patterns lie within LU_STRUCT_PAT; the component
+// LU (k_cgesv) takes any matrix and tests every group.
+constexpr uint32_t LU_STRUCT_PAT[NV] = {
+    0x7040004u, 0x7080004u, 0x7100004u, 0x7040009u, 0x7080009u, 0x7100009u, 0x7040012u, 0x7080012u,
+    0x7100012u, 0x38200020u, 0x38400020u, 0x38800020u, 0x38200041u, 0x38400041u, 0x38800041u, 0x38200082u,
+    0x38400082u, 0x38800082u, 0x7003100u, 0x7003100u, 0x7001100u, 0x7018400u, 0x7018400u, 0x7008400u,
+    0x38005200u, 0x38005200u, 0x38001200u, 0x38028800u, 0x38028800u, 0x38008800u};
+constexpr uint16_t LU_ALWAYS[NV] = {0x2000, 0x1000, 0x1800, 0xc00, 0xc00, 0xd00, 0xc00, 0x600, 0x304, 0x302,
+                                    0x184,  0x182,  0x80,   0x60,  0xc0,  0x21,  0x30,  0x30,  0x18,  0,
+                                    0,      0,      0,      0,     0,     0,     0,     0,     0,     0};
+struct LuBound { uint32_t s[NV]; };
+constexpr LuBound lu_struct_bound() {
+    LuBound b{};
+    uint32_t cur[NV] = {};
+    for (int r = 0; r < NV; r++) cur[r] = LU_STRUCT_PAT[r];
+    for (int i = 0; i < NV; i++) {
+        const uint32_t above = (0xFFFFFFFFu << (i + 1)) & ((1u << NV) - 1u);
+        uint32_t u = 0u;
+        for (int r = 0; r < NV; r++)
+            if ((cur[r] >> i) & 1u) u |= cur[r];
+        b.s[i] = u & above;
+        for (int r = 0; r < NV; r++)
+            if ((cur[r] >> i) & 1u) cur[r] |= u & above;
+    }
+    return b;
+}
+constexpr LuBound LU_BOUND = lu_struct_bound();
+enum : int { GRP_TESTED = 0, GRP_DEAD = 1, GRP_ALWAYS = 2 };
+template <int CH>
+constexpr int lu_group_class(int I, int K) {
+    return (LU_BOUND.s[I] & LuChunks<CH>::mask(I, K)) == 0u ? GRP_DEAD
+           : ((LU_ALWAYS[I] >> K) & 1u)                     ? GRP_ALWAYS
+                                                              : GRP_TESTED;
+}
+template <int CH>
+constexpr bool lu_classes_consistent() {   // no measured-always group is provably dead
+    for (int i = 0; i < NV - 1; i++)
+        for (int k = 0; k < LuChunks<CH>::count(i); k++)
+            if (((LU_ALWAYS[i] >> k) & 1u) && (LU_BOUND.s[i] & LuChunks<CH>::mask(i, k)) == 0u) return false;
+    return true;
+}
+static_assert(lu_classes_consistent<2>(), "LU_ALWAYS names a provably dead group");
+
 // Group tests on one bit: gbits = pmw | pmw >> 1 | pmw >> 2 | pmw >> 3, so bit J
 // says "some column of J..J+3 may be non-zero" and a group test is s_bitcmp1
 // + s_cbranch (the compiler keeps an s_cmp after a multi-bit s_and).
@@ -211,6 +269,18 @@ struct LuWork { unsigned long long acc, mask, groups, rare, excl; };   // mask: 
 #define HC_LU_WORK(ncols) do { } while (0)
 #define HC_LU_WORK_ARG
 #define HC_LU_WORK_PASS
+#endif
+
+#ifdef HC_DIAG_LIVE
+// diagnostic build: how often each column group of each pivot step is live
+// (wave-level test), sampled on every eighth workgroup: [I][K] live count,
+// [I][LIVE_SOLVES] sparse wave-solves that reached step I
+constexpr int LIVE_SOLVES = 16;
+__device__ unsigned long long g_diag_live[NV][LIVE_SOLVES + 1];
+#define HC_DIAG_LIVE_HIT(I, K) do { if (lane_fresh() == 0 && (blockIdx.x & 7u) == 0u) \
+    atomicAdd(&g_diag_live[I][K], 1ull); } while (0)
+#else
+#define HC_DIAG_LIVE_HIT(I, K) do { } while (0)
 #endif
 
 // the column groups K.. of step I: one uniform test per group (round 4; the
@@ -273,13 +343,14 @@ __device__ __forceinline__ void lu_store_update(cf (&rA)[NV], const cf &l, uint3
 // -5 %; a variant whose pivot row also went through a window, its address
 // exchanged with 1/pivot, issued fewer instructions and ran 1 % slower,
 // profiles/r5h_ab_lu_windows.jsonl.)
-template <int I, int K, int CH>
+template <int I, int K, int CH, bool STRUCT>
 __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32_t pmw, uint32_t gb, cf *wrow,
                                               const LUBuf &L HC_LU_WORK_ARG) {
     using C = LuChunks<CH>;
     if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
-        if (__builtin_expect(group_live<I, K, CH>(pmw, gb), 1)) {
+        constexpr int CLS = STRUCT ? lu_group_class<CH>(I, K) : GRP_TESTED;
+        if (CLS != GRP_DEAD && (CLS == GRP_ALWAYS || __builtin_expect(group_live<I, K, CH>(pmw, gb), 1))) {
             if constexpr (N == 1) {
                 wrow[J] = rA[J];
             } else {
@@ -288,6 +359,7 @@ __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32
             }
             wave_lds_sync();
             HC_LU_WORK(N);
+            HC_DIAG_LIVE_HIT(I, K);
 #ifdef HC_DIAG_LUWORK
             lu_work_acc.groups++;
 #endif
@@ -305,7 +377,7 @@ __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        lu_group_elig<I, K + 1, CH>(rA, l, pmw, gb, wrow, L HC_LU_WORK_PASS);
+        lu_group_elig<I, K + 1, CH, STRUCT>(rA, l, pmw, gb, wrow, L HC_LU_WORK_PASS);
     }
 }
 
@@ -314,7 +386,7 @@ __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32
 // finite or that met a pivot outside the fast reciprocal range): every column
 // group and the IEEE reciprocal.  The sparse solve carries no dense tests: it
 // reports such a solve, and the caller solves the system again densely.
-template <int I, bool DENSE, int CH, bool LAT>
+template <int I, bool DENSE, int CH, bool LAT, bool STRUCT>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
                                              cf *scr, bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s,
                                              bool elig HC_LU_WORK_ARG) {
@@ -381,6 +453,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
 #ifdef HC_DIAG_LUWORK
         lu_work_acc.excl = __builtin_amdgcn_ballot_w64(is_piv);
 #endif
+        HC_DIAG_LIVE_HIT(I, LIVE_SOLVES);
         if (elig) {
             HC_ISA_MARK_I("lu_mult", I);
             pf2 lq = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
@@ -388,7 +461,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
             pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-            lu_group_elig<I, 0, CH>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
+            lu_group_elig<I, 0, CH, STRUCT>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
         }
         return;
     }
@@ -411,9 +484,10 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
 // One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
 // outside the fast reciprocal range sets `redo` (the solve goes on with
 // garbage, the caller discards it and solves densely).
-template <int I, bool DENSE, int CH, bool LAT>
+template <int I, bool DENSE, int CH, bool LAT, bool STRUCT>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
-                                           bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo HC_LU_WORK_ARG) {
+                                           bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo, bool elig_in
+                                           HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
         HC_ISA_MARK_I("lu_search", I);
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
@@ -428,7 +502,10 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             reg_s = pf2{rg.x, rg.y};
             oo_s = pf2{f.o1, f.o2};
         }
-        const bool elig = rowid >= I && row_lane;
+        // eligible rows (not pivoted yet; :86-93), carried from the previous
+        // step as elig && !is_piv (SALU on the lane masks) instead of a rowid
+        // compare after the relabel (profiles/r5e1_ab.jsonl: -0.6 %)
+        const bool elig = elig_in;
         bool is_piv;
         float piv_abs;
         int pl0, pl1;   // pivot lanes of the two halves
@@ -494,9 +571,10 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             pl1 = 32 + __builtin_ctz(mhi);
         }
         HC_ISA_MARK_I("lu_pattern", I);
-        lu_step_body<I, DENSE, CH, LAT>(rA, rB, rowid, pat, my, L, scr, is_piv, pl0, pl1, reg_s, oo_s,
+        lu_step_body<I, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, my, L, scr, is_piv, pl0, pl1, reg_s, oo_s,
                                         elig HC_LU_WORK_PASS);
-        lu_forward<I + 1, DENSE, CH, LAT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scr, redo HC_LU_WORK_PASS);
+        lu_forward<I + 1, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scr, redo,
+                                          elig && !is_piv HC_LU_WORK_PASS);
     }
 }
 
@@ -553,10 +631,10 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 // rows (row r writes column group J at scratch[2r + J]); the caller's data
 // there is lost.
 constexpr int LU_SCRATCH_CF = 2 * 31 + 32;   // 94: lane r's window scratch[2r .. 2r + 31]
-template <bool DENSE, int CH = LU_CHUNK, bool LAT = false>
+template <bool DENSE, int CH = LU_CHUNK, bool LAT = false, bool STRUCT = false>
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
                                       bool &redo, unsigned long long count_mask = ~0ull);
-template <bool DENSE, int CH, bool LAT>
+template <bool DENSE, int CH, bool LAT, bool STRUCT>
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
                                       bool &redo, unsigned long long count_mask) {
     static_assert(CH == 2, "column groups of 2 (the scratch windows are 16 B)");
@@ -590,7 +668,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
     LuWork lu_work_acc{0ull, count_mask, 0ull, 0ull, 0ull};
-    lu_forward<0, DENSE, CH, LAT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, lu_work_acc);
+    lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, row_lane, lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
     if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
@@ -601,7 +679,7 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     }
     if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
-    lu_forward<0, DENSE, CH, LAT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo);
+    lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, row_lane);
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
     HC_ISA_MARK("lu_back_init");
