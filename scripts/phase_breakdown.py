@@ -30,6 +30,36 @@ def group_tests_per_solve(ch=2, nv=30):
     return n
 
 
+def _group_classes():
+    try:
+        import sys
+        import os
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+        L = _abi.lib()
+        if not hasattr(L, "hc_lu_group_class"):
+            return []
+    except Exception:   # no library here: the classes are given on the command line
+        return []
+    out = []
+    for i in range(29):
+        k = 0
+        while int(L.hc_lu_group_class(i, k)) >= 0:
+            out.append(int(L.hc_lu_group_class(i, k)))
+            k += 1
+    return out
+
+
+def always_groups():
+    """Column groups the tracker's LU runs without a test (hc_lu.hpp, class 2)."""
+    return sum(1 for c in _group_classes() if c == 2)
+
+
+def dead_groups():
+    """Column groups it never runs (class 1)."""
+    return sum(1 for c in _group_classes() if c == 1)
+
+
 def load_last_json(path):
     txt = open(path).read()
     try:
@@ -44,6 +74,9 @@ def main():
     ap.add_argument("lu_work")
     ap.add_argument("pmc")
     ap.add_argument("--out")
+    ap.add_argument("--always", type=int, default=None, help="untested always-live groups per solve "
+                    "(default: from the library's hc_lu_group_class; 0 for builds before v10.1)")
+    ap.add_argument("--dead", type=int, default=None, help="untested dead groups per solve (same default)")
     a = ap.parse_args()
     ph = load_last_json(a.isa)["phases"]
     lw = load_last_json(a.lu_work)
@@ -72,6 +105,13 @@ def main():
     live = lw["live_groups_per_wave_solve"]
     rare = lw["rare_steps_per_wave_solve"]
     tests = group_tests_per_solve()
+    # round 5 (v10.1): the always-live groups run untested (their instructions are
+    # in the ISA's fixed counts, and the LU-work count includes them) and the
+    # dead ones are gone; only the tested groups' bodies are weighted
+    n_always = a.always if a.always is not None else always_groups()
+    if n_always:
+        tests -= n_always + a.dead if a.dead is not None else n_always + dead_groups()
+        live -= n_always
     f_live = live / tests
     kinds = lw["rhs_eval_kinds"]
     kt = sum(kinds.values())
@@ -118,7 +158,9 @@ def main():
            "inputs": {"isa": a.isa, "lu_work": a.lu_work, "pmc": a.pmc,
                       "build_id": pmc.get("build_id"), "lu_work_build_id": lw.get("build_id")},
            "frequencies": {"wave_stages": stages, "sparse_wave_solves_per_wave_stage": round(solves, 4),
-                           "live_groups_per_wave_solve": round(live, 2), "group_tests_per_solve": tests,
+                           "live_groups_per_wave_solve": round(lw["live_groups_per_wave_solve"], 2),
+                           "always_live_groups_untested": n_always,
+                           "live_tested_groups_per_wave_solve": round(live, 2), "group_tests_per_solve": tests,
                            "live_group_fraction": round(f_live, 4), "rare_steps_per_wave_solve": round(rare, 3),
                            "rhs_eval_kinds": kinds},
            "note": "SQ_INSTS_VALU counts v_readlane as VALU; SALU excludes s_nop / s_waitcnt / branches here and "
