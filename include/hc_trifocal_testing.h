@@ -25,6 +25,12 @@ void hc_trifocal_set_ring_test(int delay_ticks);
    symbolic fill-in bound excludes it), 2 always run; -1 out of range. */
 unsigned hc_lu_struct_pattern(int row);
 int hc_lu_group_class(int step, int group);
+/* The rows that may hold column `step` at that pivot step under the fill-in
+   bound (bit r: row r), and the DPP span the tracker's pivot search reduces
+   over there: 1 a quad, 2 a half-row, 3 a 16-lane row, 4 the half-wave;
+   0 / -1 out of range. */
+unsigned hc_lu_candidates(int step);
+int hc_lu_search_span(int step);
 
 #ifdef __cplusplus
 }

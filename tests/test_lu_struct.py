@@ -92,3 +92,26 @@ def test_provably_live_groups_run_unconditionally(lib, problem):
                 proven += 1
                 assert int(lib.hc_lu_group_class(i, k)) == 2, (i, k)
     assert proven == 16
+
+
+def test_pivot_search_spans_cover_the_candidate_rows(lib, problem):
+    """The tracker's pivot search at step I reduces over the DPP group that
+    holds every row that may hold column I (the others hold exact zeros)."""
+    pat = structural_patterns(problem)
+    cur = list(pat)
+    spans = []
+    for i in range(NV):
+        rows = [r for r in range(NV) if (cur[r] >> i) & 1]
+        assert int(lib.hc_lu_candidates(i)) == sum(1 << r for r in rows), i
+        lo, hi = min(rows), max(rows)
+        span = 1 if lo >> 2 == hi >> 2 else 2 if lo >> 3 == hi >> 3 else 3 if lo >> 4 == hi >> 4 else 4
+        assert int(lib.hc_lu_search_span(i)) == span, i
+        spans.append(span)
+        above = ((0xFFFFFFFF << (i + 1)) & ((1 << NV) - 1))
+        u = 0
+        for r in rows:
+            u |= cur[r]
+        for r in rows:
+            cur[r] |= u & above
+    assert spans[:18] == [3, 4, 1, 3, 4, 1, 3, 4, 2, 1, 1, 2, 3, 3, 3, 3, 3, 3] and set(spans[18:]) == {4}
+    assert int(lib.hc_lu_search_span(NV)) == -1 and int(lib.hc_lu_candidates(-1)) == 0

@@ -99,6 +99,11 @@ def lib() -> C.CDLL:
             L.hc_lu_struct_pattern.argtypes = [C.c_int]
             L.hc_lu_group_class.restype = C.c_int
             L.hc_lu_group_class.argtypes = [C.c_int, C.c_int]
+        if hasattr(L, "hc_lu_search_span"):
+            L.hc_lu_candidates.restype = C.c_uint
+            L.hc_lu_candidates.argtypes = [C.c_int]
+            L.hc_lu_search_span.restype = C.c_int
+            L.hc_lu_search_span.argtypes = [C.c_int]
         L.hc_trifocal_workspace_size.restype = C.c_size_t
         L.hc_trifocal_workspace_size_for.restype = C.c_size_t
         L.hc_trifocal_workspace_size_for.argtypes = [C.c_int]
@@ -170,7 +175,7 @@ DECLARED_SYMBOLS = (
     "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
     "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
     "hc_last_error_string", "hc_trifocal_abi_version", "hc_trifocal_set_ring_test",
-    "hc_lu_struct_pattern", "hc_lu_group_class",
+    "hc_lu_struct_pattern", "hc_lu_group_class", "hc_lu_candidates", "hc_lu_search_span",
     "hc_shared_flag_create", "hc_shared_flag_open", "hc_shared_flag_reset", "hc_shared_flag_close",
     "hc_shared_flag_memory_kind",
     "hc_read_start_sols", "hc_read_start_params", "hc_read_int_table", "hc_read_float_table",

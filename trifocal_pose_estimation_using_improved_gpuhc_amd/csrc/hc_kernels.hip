@@ -1900,6 +1900,8 @@ int hc_trifocal_abi_version(void) { return HC_TRIFOCAL_ABI_VERSION; }
 // tests only (include/hc_trifocal_testing.h): the tracker LU's structural
 // patterns and column-group classes (hc_lu.hpp)
 unsigned hc_lu_struct_pattern(int row) { return row >= 0 && row < hc::NV ? hc::LU_STRUCT_PAT[row] : 0u; }
+unsigned hc_lu_candidates(int step) { return step >= 0 && step < hc::NV ? hc::LU_BOUND.cand[step] : 0u; }
+int hc_lu_search_span(int step) { return step >= 0 && step < hc::NV ? hc::lu_search_span(step) : -1; }
 int hc_lu_group_class(int step, int group) {
     if (step < 0 || step >= hc::NV - 1 || group < 0 || group >= hc::LuChunks<2>::count(step)) return -1;
     return hc::lu_group_class<2>(step, group);
@@ -1912,9 +1914,10 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.1 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+    return "hc_trifocal gfx950 v10.2 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
            "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
-           "column groups by structural class (never-fillable groups untested, always-live groups unconditional) "
+           "column groups by structural class (never-fillable groups untested, always-live groups unconditional), "
+           "pivot search narrowed to the candidate rows' DPP group "
            "(abort kernel: latency mode without exec regions), readlane back substitution, pipelined evals over "
            "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
            "issue priority)";

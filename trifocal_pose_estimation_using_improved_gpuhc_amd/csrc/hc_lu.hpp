@@ -114,6 +114,28 @@ __device__ __forceinline__ int half_max_int_p16(int v) {
     return max((int)sw[0], (int)sw[1]);
 }
 
+// x & (c | c << 32) as two s_and_b32 with a literal (no 64-bit constant
+// materialised in SGPRs)
+template <uint32_t C>
+__device__ __forceinline__ unsigned long long and_halves(unsigned long long x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    asm("s_and_b32 %0, %0, %2\n\ts_and_b32 %1, %1, %2" : "+s"(lo), "+s"(hi) : "i"(C) : "scc");
+    return (unsigned long long)lo | ((unsigned long long)hi << 32);
+}
+// max over the DPP span of lu_search_span (4: half_max_int_p16)
+template <int SPAN>
+__device__ __forceinline__ int half_max_int_span(int v) {
+    if constexpr (SPAN >= 4) {
+        return half_max_int_p16(v);
+    } else {
+        v = max(v, dpp_i<DPP_QP_1032>(v));
+        v = max(v, dpp_i<DPP_QP_2301>(v));
+        if constexpr (SPAN >= 2) v = max(v, dpp_i<DPP_ROW_HALF_MIRROR>(v));
+        if constexpr (SPAN >= 3) v = max(v, dpp_i<DPP_ROW_MIRROR>(v));
+        return v;
+    }
+}
+
 __device__ __forceinline__ int half_min_int_p16(int v) {
     v = min(v, dpp_i<DPP_QP_1032>(v));
     v = min(v, dpp_i<DPP_QP_2301>(v));
@@ -199,7 +221,7 @@ constexpr uint32_t LU_STRUCT_PAT[NV] = {
 constexpr uint16_t LU_ALWAYS[NV] = {0x2000, 0x1000, 0x1800, 0xc00, 0xc00, 0xd00, 0xc00, 0x600, 0x304, 0x302,
                                     0x184,  0x182,  0x80,   0x60,  0xc0,  0x21,  0x30,  0x30,  0x18,  0,
                                     0,      0,      0,      0,     0,     0,     0,     0,     0,     0};
-struct LuBound { uint32_t s[NV]; };
+struct LuBound { uint32_t s[NV], cand[NV]; };   // cand[I]: the rows that may hold column I at step I
 constexpr LuBound lu_struct_bound() {
     LuBound b{};
     uint32_t cur[NV] = {};
@@ -208,7 +230,7 @@ constexpr LuBound lu_struct_bound() {
         const uint32_t above = (0xFFFFFFFFu << (i + 1)) & ((1u << NV) - 1u);
         uint32_t u = 0u;
         for (int r = 0; r < NV; r++)
-            if ((cur[r] >> i) & 1u) u |= cur[r];
+            if ((cur[r] >> i) & 1u) { u |= cur[r]; b.cand[i] |= 1u << r; }
         b.s[i] = u & above;
         for (int r = 0; r < NV; r++)
             if ((cur[r] >> i) & 1u) cur[r] |= u & above;
@@ -222,6 +244,19 @@ constexpr int lu_group_class(int I, int K) {
     return (LU_BOUND.s[I] & LuChunks<CH>::mask(I, K)) == 0u ? GRP_DEAD
            : ((LU_ALWAYS[I] >> K) & 1u)                     ? GRP_ALWAYS
                                                               : GRP_TESTED;
+}
+// The pivot search of the tracker's step I need only reduce over the lanes
+// (rows) that may hold column I: every other row's entry is an exact zero.
+// Span of the DPP reduction that covers them: 1 a quad (two quad_perm
+// steps), 2 a half-row (+ row_half_mirror), 3 a 16-lane row (+ row_mirror),
+// 4 the half-wave (+ v_permlane16_swap).  Steps 0..17 need 1 to 3.
+constexpr int lu_search_span(int I) {
+    const uint32_t c = LU_BOUND.cand[I];
+    if (c == 0u) return 4;
+    int lo = 0, hi = 31;
+    while (!((c >> lo) & 1u)) lo++;
+    while (!((c >> hi) & 1u)) hi--;
+    return (lo >> 2) == (hi >> 2) ? 1 : (lo >> 3) == (hi >> 3) ? 2 : (lo >> 4) == (hi >> 4) ? 3 : 4;
 }
 template <int CH>
 constexpr bool lu_classes_consistent() {   // no measured-always group is provably dead
@@ -486,8 +521,8 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
 // garbage, the caller discards it and solves densely).
 template <int I, bool DENSE, int CH, bool LAT, bool STRUCT>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
-                                           bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo, bool elig_in
-                                           HC_LU_WORK_ARG) {
+                                           bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo,
+                                           unsigned long long elig_m HC_LU_WORK_ARG) {
     if constexpr (I < NV) {
         HC_ISA_MARK_I("lu_search", I);
         const float v = __builtin_fabsf(rA[I].x) + __builtin_fabsf(rA[I].y);          // :55
@@ -503,16 +538,29 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             oo_s = pf2{f.o1, f.o2};
         }
         // eligible rows (not pivoted yet; :86-93), carried from the previous
-        // step as elig && !is_piv (SALU on the lane masks) instead of a rowid
-        // compare after the relabel (profiles/r5e1_ab.jsonl: -0.6 %)
-        const bool elig = elig_in;
+        // step as a lane mask, elig & ~pivots (SALU), instead of a rowid
+        // compare after the relabel (profiles/r5e1_ab_lu_elig_carry.jsonl: -0.6 %)
+        const bool elig = __builtin_amdgcn_inverse_ballot_w64(elig_m);
         bool is_piv;
         float piv_abs;
         int pl0, pl1;   // pivot lanes of the two halves
+        unsigned long long piv_m;   // the two pivot lanes
+        // the tracker's steps 0..17 reduce over the candidate rows' quad,
+        // half-row or row only (lu_search_span): every other row's entry is an
+        // exact zero (key 0, or -1 when not eligible), so the candidates'
+        // group holds the maximum whenever it is a fast-range (positive) key,
+        // and the ballots keep the candidate lanes only (other groups match
+        // their own maxima).  bad == 0 then means each half's maximum is a
+        // candidate's, so popcount(m) == 2 is still one pivot per half.
+        constexpr int SPAN = (STRUCT && !DENSE) ? lu_search_span(I) : 4;
         const int key = elig ? __float_as_int(v) : -1;
-        const int mx = half_max_int_p16(key);
-        const unsigned long long m = __builtin_amdgcn_ballot_w64(key == mx);
-        const unsigned long long bad = __builtin_amdgcn_ballot_w64(!rcp_fast_bits(mx));
+        const int mx = half_max_int_span<SPAN>(key);
+        unsigned long long m = __builtin_amdgcn_ballot_w64(key == mx);
+        unsigned long long bad = __builtin_amdgcn_ballot_w64(!rcp_fast_bits(mx));
+        if constexpr (SPAN < 4) {
+            m = and_halves<LU_BOUND.cand[I]>(m);
+            bad = and_halves<LU_BOUND.cand[I]>(bad);
+        }
         const unsigned mlo = (unsigned)m, mhi = (unsigned)(m >> 32);
         // common: one maximum per half (two in the wave; s_bcnt1, where the
         // per-half m & (m - 1) tests took six SALU), both in the fast range
@@ -532,9 +580,13 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             const unsigned long long nanb = __builtin_amdgcn_ballot_w64(isn);
             // the maximum over the non-NaN candidates: the first search's unless
             // some lane holds a NaN (ties and out-of-range pivots need no second
-            // reduction)
+            // reduction) or the search was narrowed to the candidate rows
             int mx2 = mx;
             unsigned long long m2 = m;
+            if constexpr (SPAN < 4) {
+                mx2 = half_max_int_p16(key);
+                m2 = __builtin_amdgcn_ballot_w64(key == mx2);
+            }
             if (__builtin_expect(nanb != 0ull, 0)) {
                 const int key2 = (elig && !isn) ? __float_as_int(v) : -1;
                 mx2 = half_max_int_p16(key2);
@@ -551,6 +603,7 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             is_piv = lane == pl;
             piv_abs = mine_n ? __builtin_nanf("") : __int_as_float(mx2);
             const unsigned long long pm = __builtin_amdgcn_ballot_w64(is_piv);
+            piv_m = pm;
             pl0 = __builtin_ctz((unsigned)pm | 0x80000000u);
             pl1 = 32 + __builtin_ctz((unsigned)(pm >> 32) | 0x80000000u);
             if constexpr (!DENSE)
@@ -562,19 +615,22 @@ __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uin
             is_piv = key == mx && rowid == mn;
             piv_abs = __int_as_float(mx);
             const unsigned long long w = __builtin_amdgcn_ballot_w64(is_piv);
+            piv_m = w;
             pl0 = __builtin_ctz((unsigned)w);
             pl1 = 32 + __builtin_ctz((unsigned)(w >> 32));
         } else {
-            is_piv = key == mx;
+            // (the narrowed search: only the candidate lanes' matches count)
+            is_piv = __builtin_amdgcn_inverse_ballot_w64(m);   // (one bit per half: m is the pivot mask)
+            piv_m = m;
             piv_abs = __int_as_float(mx);
             pl0 = __builtin_ctz(mlo);        // exactly one bit per half here
             pl1 = 32 + __builtin_ctz(mhi);
         }
         HC_ISA_MARK_I("lu_pattern", I);
         lu_step_body<I, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, my, L, scr, is_piv, pl0, pl1, reg_s, oo_s,
-                                        elig HC_LU_WORK_PASS);
+                                                elig HC_LU_WORK_PASS);
         lu_forward<I + 1, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scr, redo,
-                                          elig && !is_piv HC_LU_WORK_PASS);
+                                                  elig_m & ~piv_m HC_LU_WORK_PASS);
     }
 }
 
@@ -668,7 +724,8 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     PivF my{pf2{0.0f, 0.0f}};
 #ifdef HC_DIAG_LUWORK
     LuWork lu_work_acc{0ull, count_mask, 0ull, 0ull, 0ull};
-    lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, row_lane, lu_work_acc);
+    lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo,
+                                          __builtin_amdgcn_ballot_w64(row_lane), lu_work_acc);
     const unsigned long long solves = (unsigned long long)__builtin_popcountll(count_mask & __builtin_amdgcn_ballot_w64(row_lane)) / NV;
     if (lane == 0 && !DENSE && !redo) {   // sparse solves that completed, and their work
         atomicAdd(&g_diag_luwork[0], lu_work_acc.acc);
@@ -679,7 +736,8 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
     }
     if (lane == 0 && DENSE) atomicAdd(&g_diag_luwork[2], solves);   // dense (re-)solves
 #else
-    lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo, row_lane);
+    lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo,
+                                          __builtin_amdgcn_ballot_w64(row_lane));
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
     HC_ISA_MARK("lu_back_init");
