@@ -1161,7 +1161,10 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             // results, do not depend on it (only on when the pose flag is set).
             const int qp = (ph == PH_STAGE) ? qpos : 0x7FFFFFFF;
             const int m = min(__builtin_amdgcn_readlane(qp, 0), __builtin_amdgcn_readlane(qp, 32));
-            const int lvl = (int)((long long)m * 16 / a.num_paths);
+#ifndef HC_ABORT_PRIO_DIV
+#define HC_ABORT_PRIO_DIV 16
+#endif
+            const int lvl = (int)((long long)m * HC_ABORT_PRIO_DIV / a.num_paths);
             if (lvl <= 0) __builtin_amdgcn_s_setprio(3);
             else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
             else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
