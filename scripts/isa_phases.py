@@ -77,10 +77,18 @@ def analyse(lines):
     body = None
     prev_bitcmp = False
     dense = False
+    since_branch = []       # classes counted in lu_search since its last branch
     for ln in lines:
         t = ln.strip()
         m = re.match(r";HCPH (\w+)(?: (\d+))?", t)
         if m:
+            if m.group(1) == "lu_rare" and cur.endswith("lu_search") and since_branch:
+                # the rare path's first instructions, scheduled above its marker
+                # (after the search's last branch, in the block that branch skips)
+                for cls in since_branch:
+                    phases[cur]["fixed"][cls] -= 1
+                    phases[("dense_" if dense else "") + "lu_rare"]["fixed"][cls] += 1
+            since_branch = []
             cur, step = m.group(1), (int(m.group(2)) if m.group(2) else None)
             if cur in ("lu_dense", "lu_sparse"):
                 dense = cur == "lu_dense"
@@ -107,6 +115,8 @@ def analyse(lines):
             body[1][cls] += 1
         else:
             ph["fixed"][cls] += 1
+            if key.endswith("lu_search"):
+                since_branch = [] if cls == "branch" else since_branch + [cls]
         # the group test: the last SCC write before the s_cbranch_scc1 is a bit
         # test (s_bitcmp0 of one column's bit) or a two-column test (s_and_b32 of
         # the pair's bits + s_cmp_eq_u32 with 0); the scheduler may put VALU or
