@@ -1917,11 +1917,11 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.2 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+    return "hc_trifocal gfx950 v10.3 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
            "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
            "column groups by structural class (never-fillable groups untested, always-live groups unconditional), "
            "pivot search narrowed to the candidate rows' DPP group "
-           "(abort kernel: latency mode without exec regions), readlane back substitution, pipelined evals over "
+           "(abort kernel: latency mode without exec regions, always-live column groups in pairs), readlane back substitution, pipelined evals over "
            "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
            "issue priority)";
 }

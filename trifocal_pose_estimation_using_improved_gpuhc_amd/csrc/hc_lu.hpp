@@ -378,11 +378,39 @@ __device__ __forceinline__ void lu_store_update(cf (&rA)[NV], const cf &l, uint3
 // -5 %; a variant whose pivot row also went through a window, its address
 // exchanged with 1/pivot, issued fewer instructions and ran 1 % slower,
 // profiles/r5h_ab_lu_windows.jsonl.)
-template <int I, int K, int CH, bool STRUCT>
+template <int I, int K, int CH, bool STRUCT, bool PAIRS = false>
 __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32_t pmw, uint32_t gb, cf *wrow,
                                               const LUBuf &L HC_LU_WORK_ARG) {
     using C = LuChunks<CH>;
-    if constexpr (K < C::count(I)) {
+    constexpr bool PAIR = PAIRS && STRUCT && K + 1 < C::count(I) && lu_group_class<CH>(I, K) == GRP_ALWAYS &&
+                          lu_group_class<CH>(I, K + 1) == GRP_ALWAYS && C::len(I, K) == 2 && C::len(I, K + 1) == 2;
+    if constexpr (PAIR) {
+        // latency mode (the abort kernel): two always-live groups, both stores,
+        // both reads, one wait (profiles/r5lp_ttfp_lat_pairs.jsonl: time to the
+        // first pose -1.6 %; the tracking kernel measured 0.7 % slower with it,
+        // three more VGPR spills: profiles/r5st_ab_lu_group_classes.jsonl, pr1)
+        constexpr int J = C::start(I, K), J2 = C::start(I, K + 1);
+        st4(&wrow[J], rA[J], rA[J + 1]);
+        st4(&wrow[J2], rA[J2], rA[J2 + 1]);
+        wave_lds_sync();
+        HC_LU_WORK(4);
+        HC_DIAG_LIVE_HIT(I, K);
+        HC_DIAG_LIVE_HIT(I, K + 1);
+#ifdef HC_DIAG_LUWORK
+        lu_work_acc.groups += 2;
+#endif
+        cf u[4];
+        ld4(&L.row[J], u[0], u[1]);
+        ld4(&L.row[J2], u[2], u[3]);
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int c = q < 2 ? J + q : J2 + q - 2;
+            const pf2 v = pcmsub(pf2{rA[c].x, rA[c].y}, l, pf2{u[q].x, u[q].y});
+            rA[c] = cmk(v.x, v.y);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        lu_group_elig<I, K + 2, CH, STRUCT, PAIRS>(rA, l, pmw, gb, wrow, L HC_LU_WORK_PASS);
+    } else if constexpr (K < C::count(I)) {
         constexpr int J = C::start(I, K), N = C::len(I, K);
         constexpr int CLS = STRUCT ? lu_group_class<CH>(I, K) : GRP_TESTED;
         if (CLS != GRP_DEAD && (CLS == GRP_ALWAYS || __builtin_expect(group_live<I, K, CH>(pmw, gb), 1))) {
@@ -412,7 +440,7 @@ __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32
             }
         }
         __builtin_amdgcn_sched_barrier(0);
-        lu_group_elig<I, K + 1, CH, STRUCT>(rA, l, pmw, gb, wrow, L HC_LU_WORK_PASS);
+        lu_group_elig<I, K + 1, CH, STRUCT, PAIRS>(rA, l, pmw, gb, wrow, L HC_LU_WORK_PASS);
     }
 }
 
@@ -496,7 +524,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
             pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-            lu_group_elig<I, 0, CH, STRUCT>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
+            lu_group_elig<I, 0, CH, STRUCT, LAT>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
         }
         return;
     }
