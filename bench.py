@@ -83,7 +83,7 @@ def lu_executed_fraction(bid):
                               lambda d: None if "scaled" in d.get("config", "") else d.get("executed_fraction"))
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector peak (64 FLOP/clk/SIMD) == FP32 MFMA peak
 HBM_PEAK_GBS = 8000.0
-TRACK_KERNEL = "void hc::k_track<false, 5, true, false>(hc::KArgs)"
+TRACK_KERNEL = "void hc::k_track<false, 5, true, false, true>(hc::KArgs)"
 
 
 def parse():
@@ -461,7 +461,11 @@ def main():
         med_launch_s = float(np.median(launch_ms)) / 1e3
         achieved_tf = flops / med_launch_s / 1e12                  # the reference's (dense) LU
         achieved_exec_tf = None if flops_exec is None else flops_exec / med_launch_s / 1e12
-        traffic, traffic_src = traffic_bytes(TRACK_KERNEL, bid)
+        tb, traffic_src = traffic_bytes(TRACK_KERNEL, bid)
+        traffic, traffic_ns = (None, None) if tb is None else tb
+        # HBM rate: the profile's bytes over the same profile's kernel time (ADVICE r5:
+        # this run's kernel time is contended when a rehearsal pins every rank to one GPU)
+        hbm_s = None if traffic is None else ((traffic_ns or float(np.median(launch_ms)) * 1e6) / 1e9)
         alg_bytes = algorithmic_bytes(S)
         k_ms = [r_[0] for r_ in rank_ms]
         line = {
@@ -517,17 +521,18 @@ def main():
                          "traffic_source": traffic_src,
                          # north_star's "achieved HBM GB/s fraction from rocprof" (VERDICT r4 #2):
                          # the PMC bytes of this build over this run's kernel time
-                         "hbm_gbs": None if traffic is None else round(traffic / (float(np.median(launch_ms)) / 1e3) / 1e9, 3),
-                         "hbm_frac": None if traffic is None else
-                         round(traffic / (float(np.median(launch_ms)) / 1e3) / 1e9 / HBM_PEAK_GBS, 6),
+                         "hbm_gbs": None if traffic is None else round(traffic / hbm_s / 1e9, 3),
+                         "hbm_frac": None if traffic is None else round(traffic / hbm_s / 1e9 / HBM_PEAK_GBS, 6),
+                         "hbm_kernel_ms": None if traffic is None else round(hbm_s * 1e3, 4),
                          "hbm_peak_gbs": HBM_PEAK_GBS,
                          "algorithmic_bytes": alg_bytes,
                          "algorithmic_gbs": round(alg_bytes / (float(np.median(launch_ms)) / 1e3) / 1e9, 3),
                          "traffic_over_algorithmic": None if traffic is None else round(traffic / alg_bytes, 3),
                          "traffic_unit": "HBM bytes per launch of the same kernel (rocprofv3 FETCH_SIZE x2 gfx950 "
-                                         "correction + WRITE_SIZE, separate --pmc passes, scripts/profile.sh); "
+                                         "correction + WRITE_SIZE, separate --pmc passes, scripts/gpu.sh profile); "
                                          "algorithmic_bytes: the compulsory bytes of the same launch (bench.algorithmic_bytes, ~0.5 KB/path); "
-                                         "hbm_gbs / hbm_frac: traffic / this run's median kernel time, / 8 TB/s",
+                                         "hbm_gbs / hbm_frac: traffic / the same profile's average kernel time "
+                                         "(hbm_kernel_ms, its rocprofv3 kernel trace), / 8 TB/s",
                          "note": "FP32 VALU-issue/latency bound tracker kernel (no GEMM: 30x30 complex LUs of "
                                  "rank-1 updates); peak = MI355X FP32 vector peak 157.3 TF. achieved = algorithmic "
                                  "FLOPs of the launch's stages (SURVEY 8d: 104.3 kFLOP / predictor stage, 101.3 "
@@ -651,12 +656,14 @@ def algorithmic_bytes(samples):
 
 
 def traffic_bytes(kernel, bid):
-    """HBM bytes per launch of `kernel` from the PMC summary of this build
-    (PMC counters cannot be collected inside the timed run): (bytes, file) or
-    (None, reason)."""
+    """HBM bytes per launch of `kernel` and that profile's own average kernel
+    time (ns, its rocprofv3 kernel trace) from the PMC summary of this build
+    (PMC counters cannot be collected inside the timed run): ((bytes, ns), file)
+    or (None, reason)."""
     return _profiles_of_build("*_pmc_summary.json", bid,
-                              lambda d: d.get("derived", {}).get("hbm_bytes_per_launch")
-                              if d.get("kernel") == kernel else None)
+                              lambda d: (d["derived"]["hbm_bytes_per_launch"], d.get("avg_ns"))
+                              if d.get("kernel") == kernel and d.get("derived", {}).get("hbm_bytes_per_launch")
+                              else None)
 
 
 def cpu_info():

@@ -45,7 +45,7 @@ typedef enum {
     HC_ERROR_WORKSPACE = 2,       /* workspace missing or too small               */
     HC_ERROR_LAUNCH = 3,          /* hipLaunchKernel / hipMemsetAsync failed      */
     HC_ERROR_DEVICE = 4,          /* no device / unsupported device (not gfx950)  */
-    HC_ERROR_TABLE = 5            /* index table exceeds the kernel's compaction capacity */
+    HC_ERROR_TABLE = 5            /* index table invalid or beyond the kernels' compaction */
 } hcStatus;
 
 /* Optional per-path counters (one per batch id).  steps = RK4 predictor
@@ -206,11 +206,13 @@ hcStatus hc_trifocal_2op1p_30x30_track_ph(const hcTrackArgs *args, void *workspa
                         8, 5, 3, 3, 1, 1 terms (or a row of more than 6
                         entries), or a dH/dt | H row of more than 13 terms
                         whose partner row (lane ^ 16) has more than 10
-                        (Evaluations); tracker launches also
-                        when a row's dH/dx structure has an entry outside
-                        trifocal_2op1p_30x30's (the LU skips the column
-                        groups that structure can never fill; the
-                        evaluation entry points take any structure);
+                        (Evaluations).  Any dH/dx structure
+                        that compacts is tracked: trifocal_2op1p_30x30's own
+                        (or one within it) by the LU specialised to it,
+                        any other (e.g. the same system with its equations
+                        permuted) by the structure-agnostic LU -- both
+                        kernels are enqueued and the table decides on the
+                        device which one runs;
      HC_ERROR_DEVICE -- time slicing only: a suspended path could not be handed
                         over (the ring overflowed: more than 4096 re-pushes of
                         abandoned tickets in one launch; or a ring entry
@@ -269,6 +271,11 @@ const char *hc_trifocal_version(void);
    differently (version 2 appended hcAbortArgs::peer_found). */
 #define HC_TRIFOCAL_ABI_VERSION 2
 int hc_trifocal_abi_version(void);
+
+/* Test hook, declared here until ABI version 1's callers have moved to
+   include/hc_trifocal_testing.h (where it is documented); still exported. */
+void hc_trifocal_set_ring_test(int delay_ticks)
+    __attribute__((deprecated("a test hook: include hc_trifocal_testing.h")));
 
 #ifdef __cplusplus
 }

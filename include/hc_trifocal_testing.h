@@ -4,6 +4,8 @@
 #ifndef HC_TRIFOCAL_TESTING_H
 #define HC_TRIFOCAL_TESTING_H
 
+#include "hc_trifocal.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -17,6 +19,16 @@ extern "C" {
    stray call cannot make them abandon every ticket.  Read at launch time. */
 #define HC_RING_TEST_MIN_TICKS 4096
 void hc_trifocal_set_ring_test(int delay_ticks);
+
+/* The end-of-launch ring check of a sliced launch (k_ring_check) on ring
+   counters set by hand: head, tail and avail are written into the workspace's
+   time-slicing area (workspace_bytes must cover the workspace and the ring
+   counters), then the check runs on `stream`.  head != tail or avail != 0 --
+   a suspended path never resumed -- sets HC_ERROR_DEVICE
+   (hc_trifocal_workspace_status) with ring_fail = (~0, avail, tail, head) in
+   the control block.  Blocks until the counters are written. */
+hcStatus hc_trifocal_ring_check_test(void *workspace, size_t workspace_bytes, unsigned head, unsigned tail,
+                                     unsigned avail, hcStream stream);
 
 /* The tracker LU's compiled-in structure (hc_lu.hpp): row `row`'s structural
    pattern of trifocal_2op1p_30x30's dH/dx (bit c: entry (row, c) has terms),

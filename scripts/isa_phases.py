@@ -2,7 +2,7 @@
 """Static instruction counts of the tracker kernel per phase of a stage (CPU).
 
 Compiles hc_kernels.hip for gfx950 to assembly with -DHC_DIAG_ISA, whose
-HC_ISA_MARK comments split the headline kernel k_track<false, 5, true, false>
+HC_ISA_MARK comments split the headline kernel k_track<false, 5, true, false, true>
 into the phases of one stage: slot control, parking, the dH/dt | H and dH/dx
 evaluations, and, per LU pivot step I, the pivot search, the rare pivot path,
 the pivot-pattern readlanes, the pivot-row stores, the read-back + 1/pivot +
@@ -26,7 +26,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = os.path.join(ROOT, "trifocal_pose_estimation_using_improved_gpuhc_amd", "csrc", "hc_kernels.hip")
-KERNEL = "_ZN2hc7k_trackILb0ELi5ELb1ELb0EEEvNS_5KArgsE"
+KERNEL = "_ZN2hc7k_trackILb0ELi5ELb1ELb0ELb1EEEvNS_5KArgsE"
 
 
 def classify(mn):

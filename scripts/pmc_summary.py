@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a scripts/profile.sh run: per-launch PMC counters of the tracker
+"""Summarise a `scripts/gpu.sh profile` run: per-launch PMC counters of the tracker
 kernel plus derived utilisations, stamped with the build id of the library the
 run loaded (the bench line's config.build_id in the trace log), which is how
 bench.py finds the profile of its own build.  usage: pmc_summary.py TAG [out.json]"""
@@ -15,7 +15,7 @@ tag = sys.argv[1]
 base = os.path.join(ROOT, "gpurun_out")
 # the headline tracker instantiation (archived ablation and abort-mode launches
 # are other instantiations of k_track and are not mixed in)
-KNAME = os.environ.get("HC_PMC_KERNEL", "void hc::k_track<false, 5, true, false>(hc::KArgs)")
+KNAME = os.environ.get("HC_PMC_KERNEL", "void hc::k_track<false, 5, true, false, true>(hc::KArgs)")
 stats = list(csv.DictReader(open(os.path.join(base, f"{tag}_trace", "run_kernel_stats.csv"))))
 trk = [r for r in stats if r["Name"] == KNAME][0]
 out = {"tag": tag, "build_id": None, "measured_at": None, "kernel": trk["Name"], "calls": int(trk["Calls"]), "avg_ns": float(trk["AverageNs"]),

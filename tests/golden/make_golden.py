@@ -108,6 +108,40 @@ def heldout_fixture(ss, sp, U):
     print("held-out track costs", np.concatenate(costs).shape)
 
 
+HELDOUT_DATASETS = ("010", "050", "099")
+
+
+def heldout_golden(ss, sp, U, K):
+    """Config 2 on synthcurves datasets no tuning ever saw:
+    Triplet_Edgels_010 / _050 / _099 with the reference's srand(0) samples,
+    100 samples each: per-path flags / counts / hashes (and the full tracks of
+    samples 0..1), the scoring of every converged path, and the maximal-support
+    pose with its GT residuals against GT_Poses21/31 of the same dataset."""
+    for ds in HELDOUT_DATASETS:
+        loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", f"Triplet_Edgels_{ds}.txt"))
+        gt21 = O.read_floats(os.path.join(RANS, "GT_Poses21", f"GT_Poses21_{ds}.txt"), 12)
+        gt31 = O.read_floats(os.path.join(RANS, "GT_Poses31", f"GT_Poses31_{ds}.txt"), 12)
+        tgt, dif, picked = O.prepare_target_params(0, [100], loc, tan, sp)
+        tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)
+        conv_ids = np.nonzero(conv)[0]
+        scores = np.array([O.score_hypothesis(tr[b], loc, K) for b in conv_ids], dtype=np.int64).reshape(-1, 3)
+        inl, sel = O.pose_support(tr, conv, loc, K)
+        res, ok = O.pose_residuals(gt21, gt31, sel)
+        np.savez_compressed(os.path.join(HERE, f"gpuhc_ds{ds}_N100_seed0.npz"),
+                            target=tgt, diff=dif, picked=picked,
+                            conv=conv, inf=inf, steps=st["steps"].astype(np.int16),
+                            corrections=st["corrections"].astype(np.int16), hash=track_hash(tr),
+                            tracks_s01=tr[:624], counts=np.array(O.count_solutions(tr, conv, inf)),
+                            scored_ids=conv_ids.astype(np.int32), scored=scores.astype(np.int32),
+                            num_candidates=np.int32(sel["num_candidates"]),
+                            path=np.array([sel["path21"], sel["path31"]], np.int32),
+                            inliers=np.array([sel["inliers21"], sel["inliers31"]], np.int32),
+                            residuals=res, success=np.bool_(ok))
+        print(f"dataset {ds}: counts", O.count_solutions(tr, conv, inf), "passing",
+              int(scores[:, 0].sum()) if len(scores) else 0, "stages", int(4 * st["steps"].sum() + st["corrections"].sum()),
+              "candidates", sel["num_candidates"], "residuals", res, ok)
+
+
 def ph_codeopt_fixture(ss, sp, U, tgt, dif, explicit_rk=False):
     """Config 2 through the archived ..._PH_CodeOpt semantics (no depth-sign
     truncation; the archived kernel is ..._TrunPaths without :148-155), or with
@@ -161,6 +195,9 @@ def main():
         return
     if only == "heldout":
         heldout_fixture(ss, sp, U)
+        return
+    if only == "heldout_golden":
+        heldout_golden(ss, sp, U, K)
         return
     if only == "pose":
         tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)

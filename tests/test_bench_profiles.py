@@ -24,13 +24,15 @@ def test_selection_by_build_id_and_timestamp(tmp_path, monkeypatch):
     _write(tmp_path, "r9z_pmc_summary.json",
            {"build_id": "v0+other", "kernel": k, "measured_at": "2099", "derived": {"hbm_bytes_per_launch": 1}})
     _write(tmp_path, "r4aa_pmc_summary.json",
-           {"build_id": "v1+abc", "kernel": k, "measured_at": "2026-10-17T10:00", "derived": {"hbm_bytes_per_launch": 7}})
+           {"build_id": "v1+abc", "kernel": k, "measured_at": "2026-10-17T10:00", "avg_ns": 2.5e7,
+            "derived": {"hbm_bytes_per_launch": 7}})
     _write(tmp_path, "r4b_pmc_summary.json",
            {"build_id": "v1+abc", "kernel": k, "measured_at": "2026-10-17T09:00", "derived": {"hbm_bytes_per_launch": 5}})
     _write(tmp_path, "r4c_pmc_summary.json",   # same build, another kernel: skipped
            {"build_id": "v1+abc", "kernel": "other", "measured_at": "2027", "derived": {"hbm_bytes_per_launch": 3}})
     v, src = bench.traffic_bytes(k, "v1+abc")
-    assert v == 7 and src == os.path.join("profiles", "r4aa_pmc_summary.json")
+    # the bytes come with the same profile's kernel time (the HBM rate's denominator)
+    assert v == (7, 2.5e7) and src == os.path.join("profiles", "r4aa_pmc_summary.json")
     v, why = bench.traffic_bytes(k, "v1+none")
     assert v is None and "v1+none" in why
 

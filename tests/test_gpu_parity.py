@@ -168,6 +168,28 @@ def test_tracker_dense_resolve_matches_oracle(problem, oracle, samples100, track
     assert inf[312:].sum() > 600 and conv[:312].sum() > 0   # the scaled samples diverge, sample 0 converges
 
 
+def test_tracker_dense_resolve_abort_mode(problem, oracle, samples100, tracker):
+    """The dense re-solve in the abort kernel (its latency-mode LU with the
+    always-live column groups in pairs, then lu_solve<true>): the
+    2^40- and 2^70-scaled samples first, so that all 936 paths are dequeued
+    before any hypothesis can pass, then config 2's sample 0.  Every tracked
+    path equals the oracle's abort-off run bit for bit."""
+    tgt, dif, _ = samples100
+    T = np.stack([(tgt[0] * np.float32(2.0 ** 40)).astype(np.float32),
+                  (tgt[0] * np.float32(2.0 ** 70)).astype(np.float32), tgt[0]])
+    D = (T - problem.start_params[None]).astype(np.float32)
+    r = tracker.track(T, D, abort=True).host()
+    tracker.workspace_status()
+    tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, T, D, problem.unified_index)
+    tracked = r["stats"]["steps"] > 0
+    assert tracked[:624].all(), "the scaled samples' paths must all be tracked"
+    assert (r["converge"][tracked] == conv[tracked]).all() and (r["infinity"][tracked] == inf[tracked]).all()
+    assert (r["stats"]["steps"][tracked] == st["steps"][tracked]).all()
+    assert (r["stats"]["corrections"][tracked] == st["corrections"][tracked]).all()
+    assert same(r["tracks"][tracked][:, :30], tr[tracked][:, :30]).all()
+    assert inf[:624].sum() > 600
+
+
 def test_tracker_matches_golden_N100(problem, samples100, tracker):
     """Config 2 (100 samples, abort off): every flag / count / track hash equals the committed golden run."""
     import sys
@@ -433,6 +455,31 @@ def test_cli_config2_matches_golden(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
 
 
+@pytest.mark.gpu
+def test_cli_four_rounds(tmp_path):
+    """`magmaHC-main -t 4` (TEST_RANSAC_TIMES = 4; cmd/magmaHC-main.cpp:38-48):
+    round ti reads Triplet_Edgels_<ti> and GT_Poses*_<ti> and draws its samples
+    with srand(ti) (GPU_HC_Solver.cpp:252-306).  Every round writes its timing,
+    solution statistics and pose line; round 0 equals the golden counts."""
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cli = os.path.join(root, "trifocal_pose_estimation_using_improved_gpuhc_amd", "bin", "magmaHC-main")
+    shutil.copytree(os.path.join(root, "data"), os.path.join(tmp_path, "data"))
+    out = subprocess.run([cli, "-p", "trifocal_2op1p_30x30", "-d", str(tmp_path), "-t", "4"], capture_output=True,
+                         text=True, timeout=300)
+    assert out.returncode == 0, out.stdout + out.stderr
+    od = os.path.join(tmp_path, "Output_Write_Files")
+    ms = [float(v) for v in open(os.path.join(od, "GPU_Timings.txt")).read().split()]
+    assert len(ms) == 4 and min(ms) > 0
+    stats = [ln.split() for ln in open(os.path.join(od, "GPU_Sols_Statistics.txt")).read().splitlines()]
+    assert len(stats) == 4 and all(int(r[0]) > 0 for r in stats)
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    assert [int(v) for v in stats[0]] == [int(v) for v in g["counts"]]
+    assert len(open(os.path.join(od, "GPU_Pose_Results.txt")).read().splitlines()) == 4
+    assert "Running 4 rounds" in out.stdout
+
+
 def test_ph_codeopt_matches_oracle_small(problem, oracle, samples100, tracker):
     """The archived ..._PH_CodeOpt semantics (hc_trifocal_2op1p_30x30_track_ph_codeopt:
     no depth-sign truncation) on 2 samples vs the oracle, value for value."""
@@ -555,31 +602,77 @@ def test_eval_rejects_tables_without_helpers(problem):
     assert (HX == 7.0).all() and (HT == 7.0).all() and (H == 7.0).all()
 
 
-def test_tracker_rejects_structure_outside_its_lu(problem, samples100, tracker):
-    """A row-permuted system (valid and equivalent) has a dH/dx structure
-    outside the one the tracker's LU compiles in (hc_lu.hpp LU_STRUCT_PAT:
-    the column groups it never tests): the evaluation entry points take it
-    (test_eval_row_permuted_tables_match_oracle), the tracker refuses it with
-    HC_ERROR_TABLE and leaves its outputs untouched, and the problem's own
-    tables still track afterwards."""
-    import dataclasses
-    import torch
+def _outside_lu_structure(dx):
+    """Rows whose dH/dx structure has an entry outside the specialised LU's
+    (hc_lu.hpp LU_STRUCT_PAT, include/hc_trifocal_testing.h)."""
     from trifocal_pose_estimation_using_improved_gpuhc_amd import _abi
+    L = _abi.lib()
+    coef = dx.reshape(30, 8, 5, 30)[:, :, 0, :]            # [column, term, row]
+    pat = [sum(1 << c for c in range(30) if (coef[c, :, r] != 0).any()) for r in range(30)]
+    return [r for r in range(30) if pat[r] & ~int(L.hc_lu_struct_pattern(r))]
+
+
+def test_tracker_row_permuted_structure_matches_oracle(problem, oracle, samples100, ransac0):
+    """Any table the reference kernel takes is tracked.  A
+    row-permuted system (valid and equivalent) has a dH/dx structure outside
+    the one the specialised LU compiles in; k_prep_tables routes it to the
+    structure-agnostic instantiation enqueued beside the specialised one.
+    Tracking (abort off, the archived PH_CodeOpt semantics, and abort mode)
+    of 2 samples equals the oracle on the same permuted tables value for
+    value, and the problem's own table still runs the specialised kernel."""
+    import dataclasses
+
+    import torch
+
     from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker
-    perm = np.arange(30)
-    perm[0], perm[9] = 9, 0
-    dx, dt, _ = _row_permuted(problem, perm)
-    dev = torch.device("cuda:0")
-    tr = DeviceTracker(dataclasses.replace(problem, dHdx_index=dx, dHdt_index=dt), dev)
     tgt, dif, _ = samples100
-    r = tr.allocate(1)
-    tr.reset_tracks(r)
-    r.converge.fill_(7)
-    tr.launch(torch.from_numpy(tgt[:1]).to(dev), torch.from_numpy(dif[:1]).to(dev), r)
-    torch.cuda.synchronize(dev)
-    assert int(tr.L.hc_trifocal_workspace_status(ctypes.c_void_p(tr.workspace.data_ptr()))) == 5   # HC_ERROR_TABLE
-    with pytest.raises(_abi.HCError):
+    N = 2
+    for swap in ((0, 9), (5, 14)):
+        perm = np.arange(30)
+        perm[swap[0]], perm[swap[1]] = swap[1], swap[0]
+        dx, dt, U = _row_permuted(problem, perm)
+        assert _outside_lu_structure(dx), f"permutation {swap} stays within the specialised LU's structure"
+        tr = DeviceTracker(dataclasses.replace(problem, dHdx_index=dx, dHdt_index=dt), torch.device("cuda:0"))
+        tr.set_ransac_data(ransac0)
+        for truncate in (True, False):
+            r = tr.track(tgt[:N], dif[:N], truncate=truncate).host()
+            tr.workspace_status()
+            o_tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, tgt[:N], dif[:N], U,
+                                                     oracle.settings(truncate=truncate))
+            assert (r["converge"] == conv).all() and (r["infinity"] == inf).all(), (swap, truncate)
+            assert (r["stats"]["steps"] == st["steps"]).all() and (r["stats"]["corrections"] == st["corrections"]).all()
+            bad = ~same(r["tracks"][:, :30], o_tr[:, :30]).all(axis=(1, 2))
+            assert not bad.any(), f"{swap} truncate={truncate}: {bad.sum()} tracks differ"
+            if truncate:
+                ref_conv, ref_tracks = conv, o_tr
+        # abort mode: every path it tracked equals the abort-off oracle run
+        a = tr.track(tgt[:N], dif[:N], abort=True).host()
         tr.workspace_status()
-    assert (r.converge == 7).all()
-    ok = tracker.track(tgt[:1], dif[:1]).host()
-    assert ok["converge"].sum() > 0
+        tracked = a["stats"]["steps"] > 0
+        assert tracked.sum() > 0
+        assert (a["converge"][tracked] == ref_conv[tracked]).all()
+        assert same(a["tracks"][tracked][:, :30], ref_tracks[tracked][:, :30]).all()
+    assert not _outside_lu_structure(problem.dHdx_index)
+
+
+def test_ring_check_reports_an_undrained_ring(tracker):
+    """The end check of a sliced launch (k_ring_check): a ring left
+    with head != tail, or with an unclaimed entry (avail != 0), is a suspended
+    path that was never resumed: HC_ERROR_DEVICE with ring_fail = (~0, avail,
+    tail, head); a drained ring stays silent."""
+    import torch
+    L = tracker.L
+    wsb = int(L.hc_trifocal_workspace_size_for(1))
+    hs = ctypes.c_void_p(torch.cuda.current_stream(tracker.device).cuda_stream)
+    for head, tail, avail, bad in ((7, 7, 0, False), (9, 7, 0, True), (7, 7, 1, True)):
+        ws = torch.zeros(wsb, dtype=torch.uint8, device=tracker.device)
+        assert int(L.hc_trifocal_ring_check_test(ctypes.c_void_p(ws.data_ptr()), wsb, head, tail, avail, hs)) == 0
+        torch.cuda.synchronize(tracker.device)
+        st = int(L.hc_trifocal_workspace_status(ctypes.c_void_p(ws.data_ptr())))
+        cb = np.frombuffer(ws[:64].cpu().numpy().tobytes(), np.uint32)
+        if bad:
+            assert st == 4 and list(cb[8:12]) == [0xFFFFFFFF, avail, tail, head], (st, cb[8:12])
+        else:
+            assert st == 0 and (cb[8:12] == 0).all()
+    small = int(L.hc_trifocal_workspace_size())
+    assert int(L.hc_trifocal_ring_check_test(ctypes.c_void_p(ws.data_ptr()), small, 1, 0, 0, hs)) == 2

@@ -848,20 +848,22 @@ __device__ unsigned long long g_diag_phase[13];
 // ARCH: the archived ablation semantics (KArgs::truncate / explicit_rk read at
 // run time); a separate instantiation so the headline kernel carries neither
 // switch and the two show up under their own names in a kernel trace.
+// LUS: the LU's column groups classed by this problem's dH/dx structure
+// (hc_lu.hpp LU_STRUCT_PAT / LU_BOUND: never-fillable groups untested,
+// always-live groups unconditional, narrowed pivot search).  Every launch
+// enqueues both instantiations; k_prep_tables decides on the device which one
+// tracks (EvalTables::lu_struct) and the other returns at once, so a table of
+// any structure the reference kernel takes (e.g. the same system with its
+// equations permuted) tracks, through the structure-agnostic LU.
 typedef uint32_t T_hxd_t[HX_NSLOT / 2][32];
-template <bool ABORT, int MINW, bool GTAB, bool ARCH = false>
+template <bool ABORT, int MINW, bool GTAB, bool ARCH = false, bool LUS = true>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     // LU (hc_lu.hpp): the abort kernel's time to the first pose is a lone
     // path's latency, so it runs the latency mode (no exec region for the pivot
     // row; profiles/r5n_ttfp.jsonl: -2.4 %); the tracking kernels the throughput one
     constexpr int LUCH = LU_CHUNK;
     constexpr bool LULAT = ABORT;
-    // the column-group classes of this problem's structure (hc_lu.hpp; the
-    // tables' check guarantees the loaded structure lies within it)
-#ifndef HC_LU_STRUCT
-#define HC_LU_STRUCT 1
-#endif
-    constexpr bool LUSTRUCT = HC_LU_STRUCT != 0;
+    constexpr bool LUSTRUCT = LUS;
     constexpr int TAB_BYTES =
         GTAB ? 16 : (int)(sizeof(uint2) * HT_TERMS * 32 + sizeof(uint32_t) * HX_SLOT_CAP * 32 + sizeof(T_hxd_t));
     __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
@@ -870,10 +872,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     Workspace *ws = a.ws;
     const EvalTables *T = &ws->tab;
     if (ws->status != 0u) return;
-    if (LUSTRUCT && T->lu_struct != 1u) {   // a structure the tracker's LU does not cover
-        if (threadIdx.x == 0) atomicMax(&ws->status, (unsigned)HC_ERROR_TABLE);
-        return;
-    }
+    if ((T->lu_struct == 1u) != LUSTRUCT) return;   // the other instantiation tracks this table
     // time slicing: this launch's ring epoch (bumped by k_prep_tables)
     const unsigned epoch = (!ABORT && a.slice_q > 0) ? ld_rlx(&a.rq[RQ_EPOCH]) : 0u;
     const uint2 *s_ht = GTAB ? T->ht : reinterpret_cast<const uint2 *>(s_tab);
@@ -1637,8 +1636,14 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     const void *kern = abort_mode ? (const void *)k_track<true, 4, true>
                        : archived ? (const void *)k_track<false, 5, true, true>
                                   : (const void *)k_track<false, 5, true>;
+    // the structure-agnostic twin, enqueued after it: exactly one of the two
+    // tracks (EvalTables::lu_struct), the other returns at its first load
+    const void *kern_any = abort_mode ? (const void *)k_track<true, 4, true, false, false>
+                           : archived ? (const void *)k_track<false, 5, true, true, false>
+                                      : (const void *)k_track<false, 5, true, false, false>;
     const int grid = grid_for((int)((paths + 1) / 2), kern);
-    if (grid <= 0) return HC_ERROR_DEVICE;
+    const int grid_any = grid_for((int)((paths + 1) / 2), kern_any);
+    if (grid <= 0 || grid_any <= 0) return HC_ERROR_DEVICE;
     if (abort_mode) {
         k.num_edgels = ab->num_triplet_edgels;
         k.inflight_stop = ab->inflight_stop ? 1 : 0;
@@ -1650,6 +1655,9 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     }
     void *kargs[] = {&k};
     g_last_hip_error = hipLaunchKernel(kern, dim3(grid), dim3(WG_THREADS), kargs, 0, s);
+    if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
+    if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
+    g_last_hip_error = hipLaunchKernel(kern_any, dim3(grid_any), dim3(WG_THREADS), kargs, 0, s);
     if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
     if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
     if (k.rq) {   // a suspended path that was never resumed is reported, not left stale
@@ -1908,6 +1916,24 @@ int hc_lu_search_span(int step) { return step >= 0 && step < hc::NV ? hc::lu_sea
 int hc_lu_group_class(int step, int group) {
     if (step < 0 || step >= hc::NV - 1 || group < 0 || group >= hc::LuChunks<2>::count(step)) return -1;
     return hc::lu_group_class<2>(step, group);
+}
+
+hcStatus hc_trifocal_ring_check_test(void *workspace, size_t workspace_bytes, unsigned head, unsigned tail,
+                                     unsigned avail, hcStream stream) {
+    if (!workspace || workspace_bytes < hc::ws_bytes_needed() + hc::RQ_WORDS * sizeof(unsigned))
+        return HC_ERROR_WORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    unsigned *rq = (unsigned *)((char *)workspace + hc::ws_bytes_needed());
+    const unsigned v[3] = {head, tail, avail};
+    const int at[3] = {hc::RQ_HEAD, hc::RQ_TAIL, hc::RQ_AVAIL};
+    (void)hipGetLastError();
+    for (int i = 0; i < 3; i++)
+        if ((hc::g_last_hip_error = hipMemcpyAsync(rq + at[i], &v[i], sizeof(unsigned), hipMemcpyHostToDevice, s)) !=
+            hipSuccess)
+            return HC_ERROR_LAUNCH;
+    if ((hc::g_last_hip_error = hipStreamSynchronize(s)) != hipSuccess) return HC_ERROR_DEVICE;
+    hipLaunchKernelGGL(hc::k_ring_check, dim3(1), dim3(64), 0, s, (hc::Workspace *)workspace, (const unsigned *)rq);
+    return hc::launch_status(HC_ERROR_LAUNCH);
 }
 
 void hc_trifocal_set_ring_test(int delay_ticks) {
