@@ -101,8 +101,10 @@ def parse():
                     help="runs per abort semantics in the early-abort leg (median, min and max reported)")
     ap.add_argument("--abort-chunk", type=int, default=125,
                     help="samples per launch in the early-abort run (the cross-GPU flag is reduced between launches)")
-    ap.add_argument("--noisy-trials", type=int, default=10,
-                    help="config 5: RANSAC runs on sigma=1px noisy synthcurves (pose success rate); 0 disables")
+    ap.add_argument("--noisy-trials", type=int, default=30,
+                    help="config 5: RANSAC runs per size on sigma=1px noisy synthcurves (pose success rate); 0 disables")
+    ap.add_argument("--noisy-samples", default="100,300,1000",
+                    help="config 5: RANSAC samples per run (over all GPUs), comma-separated: the success-rate curve")
     ap.add_argument("--noisy-sigma", type=float, default=1.0)
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the timed steps rotate over: step i runs on stream i %% streams with its own "
@@ -593,57 +595,88 @@ def sharding_gather(sel, path_offset):
     return sharding.gather_pose_selection(sel, path_offset)
 
 
+def wilson95(k, n):
+    """Wilson 95 % score interval of a binomial proportion k / n."""
+    if n == 0:
+        return None
+    z = 1.959964
+    p = k / n
+    c = (p + z * z / (2 * n)) / (1 + z * z / n)
+    h = z * np.sqrt(p * (1 - p) / n + z * z / (4 * n * n)) / (1 + z * z / n)
+    return [round(float(c - h), 4), round(float(c + h), 4)]
+
+
 def noisy_pose_leg(args, tr, problem, data, world, rank, dev, stream):
-    """BASELINE.json config 5 (path pruning is always on in the tracker): RANSAC
-    runs of samples_per_gpu*world samples on sigma-px noisy synthcurves, one
-    noise seed per trial; each run = track + device pose support, selection
-    merged over ranks; success = the selected pose matches GT within the
-    reference's 0.1 rad / 0.1 tolerances (Evaluations.cpp:523-543)."""
+    """BASELINE.json config 5 (path pruning is always on in the tracker) as a
+    curve: for each RANSAC size in --noisy-samples (samples per run over all
+    ranks), `--noisy-trials` runs on sigma-px noisy synthcurves, one noise seed
+    and one sample draw (srand(trial)) per run; each run = track + device pose
+    support, selection merged over ranks; success = the selected pose matches
+    GT within the reference's 0.1 rad / 0.1 tolerances (Evaluations.cpp:523-543).
+    Reported per size: success rate with its Wilson 95 % interval, paths/s of
+    the track + pose phase, ms per run."""
     import torch
     import torch.distributed as dist
 
     from trifocal_pose_estimation_using_improved_gpuhc_amd import pose as P
     from trifocal_pose_estimation_using_improved_gpuhc_amd import prepare_target_params, sharding, synthcurves
-    S = args.samples
-    res = tr.allocate(S, stats=False)
-    inl = torch.empty((S * 312, 2), dtype=torch.int32, device=dev)
-    sel = torch.empty(P.SEL_BYTES, dtype=torch.uint8, device=dev)
-    ok_list, times, cands = [], [], []
-    for t in range(args.noisy_trials):
-        nd = synthcurves.noisy(data, args.noisy_sigma, synthcurves.DEFAULT_SEED + t)
-        ta, da, _ = prepare_target_params(problem, nd, seed=t, num_samples=S * world, num_gpus=world)
-        off, cnt = sharding.shard(S * world, world, rank)
-        tg = torch.from_numpy(ta[off:off + cnt]).to(dev)
-        df = torch.from_numpy(da[off:off + cnt]).to(dev)
-        tr.set_ransac_data(nd)
-        tr.reset_tracks(res)
-        torch.cuda.synchronize(dev)
+    sizes = [int(v) for v in str(args.noisy_samples).split(",") if v.strip()]
+    noisy = [synthcurves.noisy(data, args.noisy_sigma, synthcurves.DEFAULT_SEED + t) for t in range(args.noisy_trials)]
+    curve = []
+    for total in sizes:
+        off, cnt = sharding.shard(total, world, rank)
+        S = max(1, sharding.max_shard(total, world))
+        res = tr.allocate(S, stats=False)
+        inl = torch.empty((S * 312, 2), dtype=torch.int32, device=dev)
+        sel = torch.empty(P.SEL_BYTES, dtype=torch.uint8, device=dev)
+        ok_list, okc_list, times, cands = [], [], [], []
+        for t in range(args.noisy_trials):
+            nd = noisy[t]
+            ta, da, _ = prepare_target_params(problem, nd, seed=t, num_samples=total, num_gpus=world)
+            tg = torch.from_numpy(ta[off:off + cnt]).to(dev)
+            df = torch.from_numpy(da[off:off + cnt]).to(dev)
+            tr.set_ransac_data(nd)
+            tr.reset_tracks(res)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            if cnt > 0:
+                tr.launch(tg, df, res, stream=stream, num_samples=cnt)
+                P.launch_pose_support(res.tracks[:cnt * 312], res.converge[:cnt * 312], tr.edgels, tr.K,
+                                      inl[:cnt * 312], sel, stream=stream)
+            torch.cuda.synchronize(dev)
+            if world > 1:
+                dist.barrier()
+            times.append(time.perf_counter() - t0)
+            m = sharding.gather_pose_selection(sel, off * 312)
+            out, ok = P.residuals(nd, m)
+            ok_list.append(ok)
+            okc_list.append(P.success_clamped(nd, m, out))
+            cands.append(m["num_candidates"])
+        tt = float(np.sum(times))
         if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        tr.launch(tg, df, res, stream=stream)
-        P.launch_pose_support(res.tracks, res.converge, tr.edgels, tr.K, inl, sel, stream=stream)
-        torch.cuda.synchronize(dev)
-        if world > 1:
-            dist.barrier()
-        times.append(time.perf_counter() - t0)
-        m = sharding.gather_pose_selection(sel, off * 312)
-        ok_list.append(P.residuals(nd, m)[1])
-        cands.append(m["num_candidates"])
-    tt = float(np.sum(times))
-    if world > 1:
-        v = torch.tensor([tt], dtype=torch.float64, device=dev)
-        dist.all_reduce(v, op=dist.ReduceOp.MAX)
-        tt = float(v.item())
+            v = torch.tensor([tt], dtype=torch.float64, device=dev)
+            dist.all_reduce(v, op=dist.ReduceOp.MAX)
+            tt = float(v.item())
+        k = int(np.sum(ok_list))
+        curve.append({"samples_per_run": total, "trials": args.noisy_trials, "successes": k,
+                      "success_rate": round(k / args.noisy_trials, 4),
+                      "success_rate_95ci": wilson95(k, args.noisy_trials),
+                      "successes_acos_clamped": int(np.sum(okc_list)),
+                      "paths_per_s": round(312 * total * args.noisy_trials / tt, 1),
+                      "ms_per_run": round(tt / args.noisy_trials * 1e3, 3),
+                      "median_candidates": int(np.median(cands))})
+        del res, inl
     tr.set_ransac_data(data)
+    head = next((c for c in curve if c["samples_per_run"] == 100 * world), curve[0])
     return {"workload": "config 5: path pruning (depth-sign truncation, always on) + sigma=%g px noisy "
-                        "synthcurves (Triplet_Edgels_000, noise seed 20250215+trial), track + device pose "
-                        "support per RANSAC run" % args.noisy_sigma,
-            "sigma_px": args.noisy_sigma, "trials": args.noisy_trials, "samples_per_run": S * world,
-            "success_rate": round(float(np.mean(ok_list)), 4),
-            "paths_per_s": round(312 * S * world * args.noisy_trials / tt, 1),
-            "ms_per_run": round(tt / args.noisy_trials * 1e3, 3),
-            "median_candidates": int(np.median(cands))}
+                        "synthcurves (Triplet_Edgels_000, noise seed 20250215+trial, samples srand(trial)), "
+                        "track + device pose support per RANSAC run, at several RANSAC sizes" % args.noisy_sigma,
+            "sigma_px": args.noisy_sigma, "trials": args.noisy_trials,
+            "samples_per_run": head["samples_per_run"], "success_rate": head["success_rate"],
+            "paths_per_s": head["paths_per_s"], "ms_per_run": head["ms_per_run"],
+            "median_candidates": head["median_candidates"], "curve": curve}
 
 
 def algorithmic_bytes(samples):

@@ -131,7 +131,8 @@ def main():
             "solves_rerun_densely": lw.get("solves_rerun_densely"),
             "live_groups_per_wave_solve": lw.get("live_groups_per_wave_solve"),
             "executed_fraction": lw.get("executed_fraction"),
-            "pose": {"gt_match": bool(ok), "candidates": sel["num_candidates"],
+            "pose": {"gt_match": bool(ok), "gt_match_acos_clamped": pose.success_clamped(data, sel, res),
+                     "candidates": sel["num_candidates"],
                      "residuals": [round(float(v), 6) for v in res]},
             "build_id": _abi.build_id(),
             "measured_at": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())}

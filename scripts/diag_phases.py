@@ -4,7 +4,9 @@
 Needs the HC_DIAG_PHASES build loaded via HC_TRIFOCAL_LIB: every wave sums the
 shader cycles (s_memtime) it spends in each phase of a stage iteration.  Prints
 the split in cycles per wave-iteration for 1 RANSAC sample (lone waves: the
-latency of a stage) and for config 2 (100 samples, full occupancy).
+latency of a stage), for config 2 (100 samples, full occupancy) and for the
+abort kernel on 1 sample (abort1: the lone latency that sets the time to the
+first pose).
 """
 import ctypes as C
 import json
@@ -29,21 +31,23 @@ def main():
     fn.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
     dev = torch.device("cuda:0")
     problem = load_problem()
-    tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, 100)
+    data = load_ransac_data(0)
+    tgt, dif, _ = prepare_target_params(problem, data, 0, 100)
     tr = DeviceTracker(problem, dev)
+    tr.set_ransac_data(data)
     out = {}
-    for n in (1, 100):
-        r = tr.allocate(n)
+    for n, abort in ((1, False), (100, False), (1, True)):
+        r = tr.allocate(n, abort=abort)
         tt, dd = torch.from_numpy(tgt[:n]).to(dev), torch.from_numpy(dif[:n]).to(dev)
         tr.reset_tracks(r)
-        tr.launch(tt, dd, r)
+        tr.launch(tt, dd, r, abort=abort)
         torch.cuda.synchronize()
         buf = (C.c_ulonglong * 13)()
         fn(buf, 1)
         tr.reset_tracks(r)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
-        tr.launch(tt, dd, r)
+        tr.launch(tt, dd, r, abort=abort)
         b.record()
         torch.cuda.synchronize()
         fn(buf, 1)
@@ -58,7 +62,7 @@ def main():
         d["waves"] = int(waves)
         d["stages"] = stages
         d["clock_ghz_est"] = round(v[7] / waves / (d["ms"] * 1e6), 3)
-        out[f"samples_{n}"] = d
+        out[f"abort_samples_{n}" if abort else f"samples_{n}"] = d
     print(json.dumps(out))
 
 

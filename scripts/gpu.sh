@@ -12,6 +12,9 @@
 #   datasets  held-out datasets (scripts/datasets.py)-> TAG_datasets.jsonl
 #   n2        bare `bench.py --gpus 2` rehearsal, both ranks on cuda:0 -> TAG_bench_n2_rehearsal.json
 #   ab        interleaved A/B of builds: extra args NAME=lib/libX.so ... (package-relative)
+#   ttfp_ab   time to the first pose of builds NAME=lib/libX.so ... (package-relative): the abort-mode
+#             parity tests on each, then 3 interleaved rounds of scripts/ttfp.py (config 3 in both
+#             semantics, 12 runs each; the lone sample, 12 runs)      -> TAG_ttfp.jsonl
 #   phases    per-phase cycles of the HC_DIAG_PHASES build (scripts/diag_phases.py)
 #   stress    time slicing under concurrent streams (scripts/slice_stress.py: 4 cold, 4 warm, 8 cold)
 #   validate  tests,luwork,bench,profile,datasets
@@ -66,6 +69,28 @@ for step in ${STEPS//,/ }; do
       for kv in "$@"; do args="$args ${kv%%=*}=$P/${kv#*=}"; last=$P/${kv#*=}; done
       HC_TRIFOCAL_LIB=$last run ab_parity 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 200 --timeout-method thread -k "not cli" > $O/${T}_parity.log 2>&1; rc=$?; tail -3 $O/${T}_parity.log
       [ $rc -eq 0 ] && { run ab 900 python -u scripts/ab_track.py $args --rounds ${AB_ROUNDS:-3} > $O/${T}_ab.jsonl; rc=$?; cat $O/${T}_ab.jsonl; } ;;
+    ttfp_ab)
+      rc=0
+      for kv in "$@"; do
+        HC_TRIFOCAL_LIB=$P/${kv#*=} run parity_${kv%%=*} 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_parity.py -x -q -m gpu --timeout 300 --timeout-method thread -k "abort or config3 or row_permuted" > $O/${T}_parity_${kv%%=*}.log 2>&1; rc=$?; tail -1 $O/${T}_parity_${kv%%=*}.log
+        [ $rc -eq 0 ] || break
+      done
+      for rd in 0 1 2; do
+        [ $rc -eq 0 ] || break
+        for kv in "$@"; do
+          for mode in "" "--inflight" "--samples 1"; do
+            HC_TRIFOCAL_LIB=$P/${kv#*=} run ttfp 120 python scripts/ttfp.py 12 $mode > $O/${T}_tmp.json; rc=$?
+            [ $rc -eq 0 ] || break 2
+            python -c "import json,sys; d=json.load(open('$O/${T}_tmp.json')); d.update(build='${kv%%=*}', round=$rd); print(json.dumps(d))" >> $O/${T}_ttfp.jsonl
+          done
+        done
+      done
+      [ -f $O/${T}_ttfp.jsonl ] && python -c "
+import json,collections
+g=collections.defaultdict(list)
+for l in open('$O/${T}_ttfp.jsonl'):
+    d=json.loads(l); g[(d['build'],d['samples'],d['inflight_stop'])].append(d['median'])
+for k,v in sorted(g.items()): print(k, v)" ;;
     phases) HC_TRIFOCAL_LIB=$L/libhc_trifocal_phases.so run phases 300 python scripts/diag_phases.py > $O/${T}_phases.json; rc=$?; cat $O/${T}_phases.json ;;
     stress)
       run stress4 300 python scripts/slice_stress.py $O/${T}_stress4.jsonl 4 4 > /dev/null 2>&1; rc=$?

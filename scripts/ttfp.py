@@ -1,6 +1,11 @@
 #!/usr/bin/env python3
-"""Time-to-first-good-pose over repeated config-3 runs (development tool, GPU):
-1000 samples, abort on, chunks of 125; prints the per-run device times (ms)."""
+"""Time to the first good pose over repeated config-3 runs (development tool, GPU):
+SAMPLES samples (default 1000: config 3; 1: the lone-sample probe, no
+contention from other hypotheses), abort on, chunks of 125, dataset 000 with
+srand(0); prints the per-run device times (ms) and their median as one JSON line.
+
+    python scripts/ttfp.py [REPS] [--samples N] [--inflight]
+"""
 import json
 import os
 import sys
@@ -13,24 +18,28 @@ sys.path.insert(0, ROOT)
 from trifocal_pose_estimation_using_improved_gpuhc_amd import load_problem, load_ransac_data, prepare_target_params, sharding  # noqa
 from trifocal_pose_estimation_using_improved_gpuhc_amd.tracker import DeviceTracker  # noqa
 
-reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+argv = sys.argv[1:]
+reps = int(argv[0]) if argv and not argv[0].startswith("-") else 10
+n = int(argv[argv.index("--samples") + 1]) if "--samples" in argv else 1000
+inflight = "--inflight" in argv
 dev = torch.device("cuda:0")
 problem = load_problem()
 data = load_ransac_data(0)
-t, d, _ = prepare_target_params(problem, data, 0, 1000)
+t, d, _ = prepare_target_params(problem, data, 0, n)
 t, d = torch.from_numpy(t).to(dev), torch.from_numpy(d).to(dev)
 tr = DeviceTracker(problem, dev)
 tr.set_ransac_data(data)
-r = tr.allocate(1000, stats=True, abort=True)
+r = tr.allocate(n, stats=True, abort=True)
 wss = []
 out = []
 for i in range(reps + 1):
     tr.reset_tracks(r)
     torch.cuda.synchronize()
-    parts = tr.launch_abort_chunked(t, d, r, 125, wss)
+    parts = tr.launch_abort_chunked(t, d, r, 125, wss, inflight_stop=inflight)
     torch.cuda.synchronize()
     hz = tr.read_timestamps(wss[0])[2]
     f = sharding.first_found_seconds([tr.read_timestamps(x)[:2] for x in wss[:len(parts)]], hz)
     if i:
         out.append(round(f * 1e3, 3))
-print(json.dumps({"ttfp_ms": out, "median": float(np.median(out)), "min": min(out), "max": max(out)}))
+print(json.dumps({"samples": n, "inflight_stop": inflight, "ttfp_ms": out, "median": float(np.median(out)),
+                  "min": min(out), "max": max(out)}))

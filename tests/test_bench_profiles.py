@@ -46,3 +46,11 @@ def test_lu_fraction_skips_scaled_runs(tmp_path, monkeypatch):
                                         "executed_fraction": 0.42}, jsonl=True)
     v, src = bench.lu_executed_fraction("b")
     assert v == 0.42 and src.endswith("b_lu_work.json")
+
+
+def test_wilson_interval():
+    """Config 5's success-rate interval (bench.wilson95): Wilson 95 % score interval."""
+    lo, hi = bench.wilson95(6, 10)
+    assert abs(lo - 0.3127) < 1e-3 and abs(hi - 0.8318) < 1e-3
+    assert bench.wilson95(0, 30)[0] == 0.0 and bench.wilson95(30, 30)[1] == 1.0
+    assert bench.wilson95(0, 0) is None

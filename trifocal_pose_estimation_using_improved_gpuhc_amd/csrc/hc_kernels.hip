@@ -1190,9 +1190,23 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
             // steps are bounded by max_steps - stepidx, so the paths that can
             // still run longest get the larger share of their SIMD, and the
             // launch ends with evenly short remainders.
+#ifndef HC_PRIO_REM
+#define HC_PRIO_REM 0
+#endif
+#if HC_PRIO_REM
+            // A/B: longest estimated remaining work first -- the steps left at
+            // dt doubling every 4 accepted steps, 4 log2(1 + (2^1/4 - 1)(1 - t0) / dt),
+            // capped by the steps the path may still take
+            const float est = 4.0f * __builtin_amdgcn_logf(1.0f + 0.1892f * (1.0f - t0) * __builtin_amdgcn_rcpf(dt));
+            int rem = a.max_steps - stepidx;
+            rem = (ph == PH_STAGE) ? min(rem, (int)est) : -1;
+            const int mr = max(__builtin_amdgcn_readlane(rem, 0), __builtin_amdgcn_readlane(rem, 32));
+            const int q4 = 3 - (int)((long long)max(mr, 0) * 4 / (a.max_steps + 1));
+#else
             const int si = (ph == PH_STAGE) ? stepidx : (1 << 20);
             const int m = min(__builtin_amdgcn_readlane(si, 0), __builtin_amdgcn_readlane(si, 32));
             const int q4 = (int)((long long)m * 4 / (a.max_steps + 1));
+#endif
             if (q4 <= 0) __builtin_amdgcn_s_setprio(3);
             else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
             else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
@@ -1323,6 +1337,13 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 #endif
         }
         wave_lds_sync();
+#ifdef HC_DIAG_PHASES
+        {   // [4] forward elimination up to the solve's boundary stamp, [5] the rest of the LU
+            const uint64_t mid = g_diag_lu_mid[blockIdx.x * 4 + wid];
+            const uint64_t n_ = __builtin_amdgcn_s_memtime();
+            if (mid > dt_ && mid < n_) { dg[4] += mid - dt_; dt_ = mid; }
+        }
+#endif
         HC_DIAG_MARK(5);
         HC_ISA_MARK("ctl_update");
         {
@@ -1943,11 +1964,12 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.3 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+    return "hc_trifocal gfx950 v10.4 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
            "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
            "column groups by structural class (never-fillable groups untested, always-live groups unconditional), "
            "pivot search narrowed to the candidate rows' DPP group "
-           "(abort kernel: latency mode without exec regions, always-live column groups in pairs), readlane back substitution, pipelined evals over "
+           "(abort kernel: batched latency mode, one LDS round trip per pivot step, every live-able column group untested), "
+           "structure-agnostic twin kernels for other dH/dx structures, readlane back substitution, pipelined evals over "
            "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
            "issue priority)";
 }

@@ -306,6 +306,10 @@ struct LuWork { unsigned long long acc, mask, groups, rare, excl; };   // mask: 
 #define HC_LU_WORK_PASS
 #endif
 
+#ifdef HC_DIAG_PHASES
+__device__ unsigned long long g_diag_lu_mid[65536];   // per (workgroup, wave): see lu_solve
+#endif
+
 #ifdef HC_DIAG_LIVE
 // diagnostic build: how often each column group of each pivot step is live
 // (wave-level test), sampled on every eighth workgroup: [I][K] live count,
@@ -444,6 +448,88 @@ __device__ __forceinline__ void lu_group_elig(cf (&rA)[NV], const pf2 &l, uint32
     }
 }
 
+// Batched latency mode (round 6; the abort kernel with the problem's structure,
+// whose time to the first pose is a lone path's latency).  Every column group
+// the fill-in bound leaves alive (124 of 225 per solve) runs without a test --
+// a group that happens to be zero in the pivot row is exact, as for the
+// always-live groups -- so a pivot step needs no pattern bookkeeping, and it
+// makes ONE LDS round trip instead of one per live group: every lane writes
+// 1/pivot, rhs, rowid and all those groups (the pivot lane into the buffer,
+// the others into their scratch windows), then every lane reads them back
+// together, then the eligible rows update.
+#ifndef HC_LU_LATB
+#define HC_LU_LATB 1
+#endif
+template <int CH>
+struct LatCols {   // the columns of step I's live-able groups, packed in group order
+    static constexpr int off(int I, int K) {
+        int n = 0;
+        for (int k = 0; k < K; k++)
+            if (lu_group_class<CH>(I, k) != GRP_DEAD) n += LuChunks<CH>::len(I, k);
+        return n;
+    }
+    static constexpr int total(int I) { return off(I, LuChunks<CH>::count(I)); }
+};
+template <int I, int K, int CH>
+__device__ __forceinline__ void lat_store(const cf (&rA)[NV], cf *wrow) {
+    using C = LuChunks<CH>;
+    if constexpr (K < C::count(I)) {
+        if constexpr (lu_group_class<CH>(I, K) != GRP_DEAD) {
+            constexpr int J = C::start(I, K), N = C::len(I, K);
+            if constexpr (N == 1) wrow[J] = rA[J];
+            else st4(&wrow[J], rA[J], rA[J + 1]);
+        }
+        lat_store<I, K + 1, CH>(rA, wrow);
+    }
+}
+// the groups whose packed columns start in [LO, HI) (a batch: its reads are
+// issued together, its updates follow)
+template <int I, int K, int CH, int LO, int HI, int M>
+__device__ __forceinline__ void lat_load(cf (&u)[M], const LUBuf &L) {
+    using C = LuChunks<CH>;
+    if constexpr (K < C::count(I)) {
+        constexpr int O = LatCols<CH>::off(I, K);
+        if constexpr (lu_group_class<CH>(I, K) != GRP_DEAD && O >= LO && O < HI) {
+            constexpr int J = C::start(I, K), N = C::len(I, K);
+            if constexpr (N == 1) u[O - LO] = L.row[J];
+            else ld4(&L.row[J], u[O - LO], u[O - LO + 1]);
+        }
+        lat_load<I, K + 1, CH, LO, HI>(u, L);
+    }
+}
+template <int I, int K, int CH, int LO, int HI, int M>
+__device__ __forceinline__ void lat_fma(cf (&rA)[NV], const pf2 &l, const cf (&u)[M]) {
+    using C = LuChunks<CH>;
+    if constexpr (K < C::count(I)) {
+        constexpr int O = LatCols<CH>::off(I, K);
+        if constexpr (lu_group_class<CH>(I, K) != GRP_DEAD && O >= LO && O < HI) {
+            constexpr int J = C::start(I, K), N = C::len(I, K);
+#pragma unroll
+            for (int q = 0; q < N; q++) {
+                const pf2 v = pcmsub(pf2{rA[J + q].x, rA[J + q].y}, l, pf2{u[O - LO + q].x, u[O - LO + q].y});
+                rA[J + q] = cmk(v.x, v.y);
+            }
+        }
+        lat_fma<I, K + 1, CH, LO, HI>(rA, l, u);
+    }
+}
+// columns read in the step's first batch (with 1/pivot and rhs); the rest
+// follow in batches of the same size (the abort kernel has 128 VGPRs)
+#ifndef HC_LU_LATB_COLS
+#define HC_LU_LATB_COLS 8
+#endif
+template <int I, int LO, int CH>
+__device__ __forceinline__ void lat_batches(cf (&rA)[NV], const pf2 &l, const LUBuf &L) {
+    constexpr int T = LatCols<CH>::total(I);
+    if constexpr (LO < T) {
+        constexpr int HI = LO + HC_LU_LATB_COLS;
+        cf u[HC_LU_LATB_COLS + 1];
+        lat_load<I, 0, CH, LO, HI>(u, L);
+        lat_fma<I, 0, CH, LO, HI>(rA, l, u);
+        lat_batches<I, HI, CH>(rA, l, L);
+    }
+}
+
 // The rest of pivot step I once the pivots are chosen: broadcast, relabel,
 // 1/pivot, update.  DENSE (the whole solve of a matrix that is not provably
 // finite or that met a pivot outside the fast reciprocal range): every column
@@ -453,6 +539,36 @@ template <int I, bool DENSE, int CH, bool LAT, bool STRUCT>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
                                              cf *scr, bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s,
                                              bool elig HC_LU_WORK_ARG) {
+    if constexpr (HC_LU_LATB && LAT && STRUCT && CH == 2 && !DENSE) {
+        HC_ISA_MARK_I("lu_store", I);
+        cf *wrow = is_piv ? L.row : scr;
+        wrow[I] = cmk(reg_s.x, reg_s.y);
+        st4(&wrow[30], rB, cmk(__int_as_float(rowid), 0.0f));
+        lat_store<I, 0, CH>(rA, wrow);
+        wave_lds_sync();
+        HC_ISA_MARK_I("lu_rcp", I);
+        const cf reg = L.row[I];
+        cf sB0, pr;
+        ld4(&L.row[30], sB0, pr);
+        cf u[HC_LU_LATB_COLS + 1];
+        lat_load<I, 0, CH, 0, HC_LU_LATB_COLS>(u, L);
+        const int piv_pos = __float_as_int(pr.x);
+        rowid = is_piv ? I : (rowid == I ? piv_pos : rowid);   // :70-82
+        my.oo.x = is_piv ? oo_s.x : my.oo.x;
+        my.oo.y = is_piv ? oo_s.y : my.oo.y;
+        asm volatile("" : "+v"(my.oo));
+        HC_ISA_MARK_I("lu_update", I);
+        if (elig) {   // the rows below and the pivot row (multiplier 0: unchanged up to the sign of zeros)
+            HC_ISA_MARK_I("lu_mult", I);
+            const pf2 lq = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+            const pf2 lp = {is_piv ? 0.0f : lq.x, is_piv ? 0.0f : lq.y};
+            const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
+            rB = cmk(bp.x, bp.y);
+            lat_fma<I, 0, CH, 0, HC_LU_LATB_COLS>(rA, lp, u);
+            lat_batches<I, HC_LU_LATB_COLS, CH>(rA, lp, L);
+        }
+        return;
+    }
     constexpr uint32_t FULL = 0xFFFFFFFFu << (I + 1);
     uint32_t pmw = FULL;
     if constexpr (!DENSE) {
@@ -766,6 +882,11 @@ __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t p
 #else
     lu_forward<0, DENSE, CH, LAT, STRUCT>(rA, rB, rowid, pat, lane, r, hb, row_lane, my, L, scratch + 2 * r, redo,
                                           __builtin_amdgcn_ballot_w64(row_lane));
+#endif
+#ifdef HC_DIAG_PHASES
+    // diagnostic build: the forward / back-substitution boundary of this wave's
+    // solve (s_memtime), read by k_track after the solve (g_diag_lu_mid)
+    if ((lane & 63) == 0 && blockIdx.x < 16384u) g_diag_lu_mid[blockIdx.x * 4 + (threadIdx.x >> 6)] = __builtin_amdgcn_s_memtime();
 #endif
     // lane r returns x_r (captured at back-substitution step r; padding lanes 0)
     HC_ISA_MARK("lu_back_init");

@@ -89,3 +89,17 @@ def residuals(data: RansacData, sel: dict):
                                                         sel["R31"], sel["t31"])]
     ok = _abi.lib().hc_pose_residuals(*[C.c_void_p(v.ctypes.data) for v in a], C.c_void_p(out.ctypes.data))
     return out, bool(ok)
+
+
+def success_clamped(data: RansacData, sel: dict, out: np.ndarray) -> bool:
+    """The GT verdict with the rotation residual's acos argument clamped to
+    [-1, 1].  The reference (Evaluations.cpp:360-374) does not clamp: an exact
+    rotation whose float trace rounds above 3 gives acos(> 1) = NaN, and the
+    pose counts as a failure.  Reported beside the reference verdict, never
+    instead of it."""
+    rot = []
+    for gt, R in ((data.pose21, sel["R21"]), (data.pose31, sel["R31"])):
+        G = np.asarray(gt, np.float64)[:9].reshape(3, 3)
+        M = G.T @ np.asarray(R, np.float64).reshape(3, 3)
+        rot.append(float(np.arccos(np.clip(0.5 * (np.trace(M) - 1.0), -1.0, 1.0))))
+    return bool(rot[0] < 0.1 and rot[1] < 0.1 and float(out[2]) < 0.1 and float(out[3]) < 0.1)
