@@ -862,7 +862,7 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     // path's latency, so it runs the latency mode (no exec region for the pivot
     // row; profiles/r5n_ttfp.jsonl: -2.4 %); the tracking kernels the throughput one
     constexpr int LUCH = LU_CHUNK;
-    constexpr bool LULAT = ABORT;
+    constexpr int LULAT = ABORT ? HC_LU_LATB_COLS : 0;
     constexpr bool LUSTRUCT = LUS;
     constexpr int TAB_BYTES =
         GTAB ? 16 : (int)(sizeof(uint2) * HT_TERMS * 32 + sizeof(uint32_t) * HX_SLOT_CAP * 32 + sizeof(T_hxd_t));

@@ -514,19 +514,20 @@ __device__ __forceinline__ void lat_fma(cf (&rA)[NV], const pf2 &l, const cf (&u
     }
 }
 // columns read in the step's first batch (with 1/pivot and rhs); the rest
-// follow in batches of the same size (the abort kernel has 128 VGPRs)
+// follow in batches of the same size: the lu_solve template parameter LAT
+// (the abort kernel has 128 VGPRs: 8, profiles/r6c_ttfp_ab_latb_cols.jsonl)
 #ifndef HC_LU_LATB_COLS
 #define HC_LU_LATB_COLS 8
 #endif
-template <int I, int LO, int CH>
+template <int I, int LO, int CH, int B>
 __device__ __forceinline__ void lat_batches(cf (&rA)[NV], const pf2 &l, const LUBuf &L) {
     constexpr int T = LatCols<CH>::total(I);
     if constexpr (LO < T) {
-        constexpr int HI = LO + HC_LU_LATB_COLS;
-        cf u[HC_LU_LATB_COLS + 1];
+        constexpr int HI = LO + B;
+        cf u[B + 1];
         lat_load<I, 0, CH, LO, HI>(u, L);
         lat_fma<I, 0, CH, LO, HI>(rA, l, u);
-        lat_batches<I, HI, CH>(rA, l, L);
+        lat_batches<I, HI, CH, B>(rA, l, L);
     }
 }
 
@@ -535,11 +536,11 @@ __device__ __forceinline__ void lat_batches(cf (&rA)[NV], const pf2 &l, const LU
 // finite or that met a pivot outside the fast reciprocal range): every column
 // group and the IEEE reciprocal.  The sparse solve carries no dense tests: it
 // reports such a solve, and the caller solves the system again densely.
-template <int I, bool DENSE, int CH, bool LAT, bool STRUCT>
+template <int I, bool DENSE, int CH, int LAT, bool STRUCT>
 __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, PivF &my, LUBuf &L,
                                              cf *scr, bool is_piv, int pl0, int pl1, pf2 reg_s, pf2 oo_s,
                                              bool elig HC_LU_WORK_ARG) {
-    if constexpr (HC_LU_LATB && LAT && STRUCT && CH == 2 && !DENSE) {
+    if constexpr (HC_LU_LATB && LAT > 0 && STRUCT && CH == 2 && !DENSE) {
         HC_ISA_MARK_I("lu_store", I);
         cf *wrow = is_piv ? L.row : scr;
         wrow[I] = cmk(reg_s.x, reg_s.y);
@@ -550,8 +551,8 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         const cf reg = L.row[I];
         cf sB0, pr;
         ld4(&L.row[30], sB0, pr);
-        cf u[HC_LU_LATB_COLS + 1];
-        lat_load<I, 0, CH, 0, HC_LU_LATB_COLS>(u, L);
+        cf u[LAT + 1];
+        lat_load<I, 0, CH, 0, LAT>(u, L);
         const int piv_pos = __float_as_int(pr.x);
         rowid = is_piv ? I : (rowid == I ? piv_pos : rowid);   // :70-82
         my.oo.x = is_piv ? oo_s.x : my.oo.x;
@@ -564,8 +565,8 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
             const pf2 lp = {is_piv ? 0.0f : lq.x, is_piv ? 0.0f : lq.y};
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
-            lat_fma<I, 0, CH, 0, HC_LU_LATB_COLS>(rA, lp, u);
-            lat_batches<I, HC_LU_LATB_COLS, CH>(rA, lp, L);
+            lat_fma<I, 0, CH, 0, LAT>(rA, lp, u);
+            lat_batches<I, LAT, CH, LAT>(rA, lp, L);
         }
         return;
     }
@@ -583,7 +584,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
     // the buffer, the others to their scratch windows -- no exec region, at the
     // price of LDS bandwidth (profiles/r5m_ab_lu_x.jsonl: lone sample -2 %,
     // loaded launch +0.8 %)
-    constexpr bool X1 = LAT && CH == 2 && !DENSE;
+    constexpr bool X1 = LAT > 0 && CH == 2 && !DENSE;
     cf *wrow = nullptr;
     if constexpr (X1) {
         wrow = is_piv ? L.row : scr;
@@ -640,7 +641,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
             pat |= (uint32_t)__builtin_amdgcn_sbfe((int)pat, I, 1) & pmw;
-            lu_group_elig<I, 0, CH, STRUCT, LAT>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
+            lu_group_elig<I, 0, CH, STRUCT, (LAT > 0)>(rA, lp, pmw, gb, wrow, L HC_LU_WORK_PASS);
         }
         return;
     }
@@ -663,7 +664,7 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
 // One pivot step: the pivot search, then lu_step_body.  !DENSE: a pivot
 // outside the fast reciprocal range sets `redo` (the solve goes on with
 // garbage, the caller discards it and solves densely).
-template <int I, bool DENSE, int CH, bool LAT, bool STRUCT>
+template <int I, bool DENSE, int CH, int LAT, bool STRUCT>
 __device__ __forceinline__ void lu_forward(cf (&rA)[NV], cf &rB, int &rowid, uint32_t &pat, int lane, int r, int hb,
                                            bool row_lane, PivF &my, LUBuf &L, cf *scr, bool &redo,
                                            unsigned long long elig_m HC_LU_WORK_ARG) {
@@ -831,10 +832,10 @@ __device__ __forceinline__ void lu_backward(const cf (&rA)[NV], cf &rB, int rowi
 // rows (row r writes column group J at scratch[2r + J]); the caller's data
 // there is lost.
 constexpr int LU_SCRATCH_CF = 2 * 31 + 32;   // 94: lane r's window scratch[2r .. 2r + 31]
-template <bool DENSE, int CH = LU_CHUNK, bool LAT = false, bool STRUCT = false>
+template <bool DENSE, int CH = LU_CHUNK, int LAT = 0, bool STRUCT = false>
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
                                       bool &redo, unsigned long long count_mask = ~0ull);
-template <bool DENSE, int CH, bool LAT, bool STRUCT>
+template <bool DENSE, int CH, int LAT, bool STRUCT>
 __device__ __forceinline__ cf lu_solve(cf (&rA)[NV], cf rB, int lane, uint32_t pattern, LUBuf &L, cf *scratch,
                                       bool &redo, unsigned long long count_mask) {
     static_assert(CH == 2, "column groups of 2 (the scratch windows are 16 B)");

@@ -36,8 +36,10 @@ struct alignas(16) SlotLDS {
     cf x[32];        // current track (x[30] = 1)
     cf xl[32];       // last successful track
     cf sols[32];     // RK accumulator
-    cf ent[ENT_CAP]; // dH/dx entries, packed (k_prep_tables; kept through the LU); p(t) and the
-                     // diff params are staged in its first 68 entries while the prefixes are built
+    cf ent[ENT_CAP]; // dH/dx entries, packed (k_prep_tables); p(t) and the diff params are staged
+                     // in its first 68 entries while the prefixes are built.  The sparse LU
+                     // overwrites ent[0 .. LU_SCRATCH_CF) with its store windows (hc_lu.hpp): after
+                     // a solve only the structural zero at ENT_CAP - 1 is intact
     cf lu[32];       // the LU's pivot-row buffer (hc_lu.hpp LUBuf)
     cf tp[TP_CAP];   // prefix table T: (c * p[a]) * p[b] per (c, a, b) triple (dH/dx and H terms)
     cf qp[QP_CAP];   // prefix table Q: d[a] * p[b] + d[b] * p[a] per (a, b) pair (dH/dt terms)
