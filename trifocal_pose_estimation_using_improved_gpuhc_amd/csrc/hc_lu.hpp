@@ -153,7 +153,9 @@ struct PivF { pf2 oo; };
 // cuCdivf(1, y) for s = |y.re| + |y.im| in the fast range, in packed FP32 with
 // the spec's ops: o1 = 1/s, (brs, bis) = y*o1, o2 = 1/(brs*brs + bis*bis),
 // 1/y = ((o1*brs)*o2, (-(o1*bis))*o2); -(o1*bis) is computed as o1*(-bis)
-// (IEEE: the same value).  oo returns (o1, o2).
+// (IEEE: the same value).  oo returns (o1, o2).  (Computing o2 straight into
+// the high half of o1's pair saves the pivot lane one move per step but
+// raised the tracking kernel's spills from 11 to 53 VGPRs; round 6.)
 __device__ __forceinline__ pf2 recip_fast(pf2 y, float s, pf2 &oo) {
     // o1 and o2 each in a pair of their own (low half), broadcast by op_sel:
     // no copy to place them side by side
@@ -548,6 +550,9 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         lat_store<I, 0, CH>(rA, wrow);
         wave_lds_sync();
         HC_ISA_MARK_I("lu_rcp", I);
+        // (the pivot lane reading an exact zero from a zero slot instead, so that
+        // its multiplier needs no selects, issued fewer instructions and measured
+        // no faster: profiles/r6f_ttfp_ab_zero_slot.jsonl)
         const cf reg = L.row[I];
         cf sB0, pr;
         ld4(&L.row[30], sB0, pr);
@@ -636,7 +641,10 @@ __device__ __forceinline__ void lu_step_body(cf (&rA)[NV], cf &rB, int &rowid, u
         HC_DIAG_LIVE_HIT(I, LIVE_SOLVES);
         if (elig) {
             HC_ISA_MARK_I("lu_mult", I);
-            pf2 lq = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
+            // (the pivot lane's multiplier is zeroed by two selects: reading an
+            // exact zero from a zero slot instead held one more address in a VGPR
+            // across the solve: 11 -> 20 spills; round 6)
+            const pf2 lq = pcmul(pf2{rA[I].x, rA[I].y}, pf2{reg.x, reg.y});
             const pf2 lp = {is_piv ? 0.0f : lq.x, is_piv ? 0.0f : lq.y};
             const pf2 bp = pcmsub(pf2{rB.x, rB.y}, lp, pf2{sB0.x, sB0.y});
             rB = cmk(bp.x, bp.y);
