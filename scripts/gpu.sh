@@ -18,7 +18,8 @@
 #   phases    per-phase cycles of the HC_DIAG_PHASES build (scripts/diag_phases.py)
 #   stress    time slicing under concurrent streams (scripts/slice_stress.py: 4 cold, 4 warm, 8 cold)
 #   validate  tests,luwork,bench,profile,datasets
-# Extra environment: BENCH_ARGS (bench step), AB_ROUNDS (ab step, default 3).
+# Extra environment: BENCH_ARGS (bench step), AB_ROUNDS (ab step, default 3), TTFP_ARGS (ttfp_ab step,
+# e.g. "--dataset 10").
 export TMPDIR=/tmp
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
 STEPS=$1; T=$2; shift 2
@@ -79,7 +80,7 @@ for step in ${STEPS//,/ }; do
         [ $rc -eq 0 ] || break
         for kv in "$@"; do
           for mode in "" "--inflight" "--samples 1"; do
-            HC_TRIFOCAL_LIB=$P/${kv#*=} run ttfp 120 python scripts/ttfp.py 12 $mode > $O/${T}_tmp.json; rc=$?
+            HC_TRIFOCAL_LIB=$P/${kv#*=} run ttfp 120 python scripts/ttfp.py 12 $mode $TTFP_ARGS > $O/${T}_tmp.json; rc=$?
             [ $rc -eq 0 ] || break 2
             python -c "import json,sys; d=json.load(open('$O/${T}_tmp.json')); d.update(build='${kv%%=*}', round=$rd); print(json.dumps(d))" >> $O/${T}_ttfp.jsonl
           done

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Time to the first good pose over repeated config-3 runs (development tool, GPU):
 SAMPLES samples (default 1000: config 3; 1: the lone-sample probe, no
-contention from other hypotheses), abort on, chunks of 125, dataset 000 with
-srand(0); prints the per-run device times (ms) and their median as one JSON line.
+contention from other hypotheses), abort on, chunks of 125, dataset K (000)
+with srand(0); prints the per-run device times (ms) and their median as one JSON line.
 
-    python scripts/ttfp.py [REPS] [--samples N] [--inflight]
+    python scripts/ttfp.py [REPS] [--samples N] [--inflight] [--dataset K]
 """
 import json
 import os
@@ -22,9 +22,10 @@ argv = sys.argv[1:]
 reps = int(argv[0]) if argv and not argv[0].startswith("-") else 10
 n = int(argv[argv.index("--samples") + 1]) if "--samples" in argv else 1000
 inflight = "--inflight" in argv
+ds = int(argv[argv.index("--dataset") + 1]) if "--dataset" in argv else 0
 dev = torch.device("cuda:0")
 problem = load_problem()
-data = load_ransac_data(0)
+data = load_ransac_data(ds)
 t, d, _ = prepare_target_params(problem, data, 0, n)
 t, d = torch.from_numpy(t).to(dev), torch.from_numpy(d).to(dev)
 tr = DeviceTracker(problem, dev)
@@ -41,5 +42,5 @@ for i in range(reps + 1):
     f = sharding.first_found_seconds([tr.read_timestamps(x)[:2] for x in wss[:len(parts)]], hz)
     if i:
         out.append(round(f * 1e3, 3))
-print(json.dumps({"samples": n, "inflight_stop": inflight, "ttfp_ms": out, "median": float(np.median(out)),
+print(json.dumps({"samples": n, "dataset": ds, "inflight_stop": inflight, "ttfp_ms": out, "median": float(np.median(out)),
                   "min": min(out), "max": max(out)}))

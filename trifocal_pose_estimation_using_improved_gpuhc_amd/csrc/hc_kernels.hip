@@ -364,10 +364,25 @@ __global__ void __launch_bounds__(PREP_THREADS) k_prep_tables(PrepArgs pa) {
     __shared__ int s_valid;
     const int tid = threadIdx.x;
     {
+        // the table's hash (a sum, so any load order gives it): 16-B loads when
+        // the caller's table is 16-B aligned (the per-launch check took 40 us
+        // with one int per load, a fifth of the launch overhead; round 6)
         unsigned long long h = 0;
+        if (((uintptr_t)U & 15u) == 0u) {
+            const int4 *U4 = reinterpret_cast<const int4 *>(U);
+            static_assert((HX_SIZE + HT_SIZE) % 4 == 0, "whole int4 words");
+#pragma unroll 4
+            for (int i = tid; i < (HX_SIZE + HT_SIZE) / 4; i += PREP_THREADS) {
+                const int4 v = U4[i];
+                const unsigned long long b = (unsigned long long)(4 * i) << 32;
+                h += mix64(b | (unsigned)v.x) + mix64((b + (1ull << 32)) | (unsigned)v.y) +
+                     mix64((b + (2ull << 32)) | (unsigned)v.z) + mix64((b + (3ull << 32)) | (unsigned)v.w);
+            }
+        } else {
 #pragma unroll 8
-        for (int i = tid; i < HX_SIZE + HT_SIZE; i += PREP_THREADS)
-            h += mix64(((unsigned long long)i << 32) | (unsigned)U[i]);
+            for (int i = tid; i < HX_SIZE + HT_SIZE; i += PREP_THREADS)
+                h += mix64(((unsigned long long)i << 32) | (unsigned)U[i]);
+        }
         s_h[tid] = h;
     }
     if (tid == 0) {
@@ -1654,12 +1669,18 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     // (time to the first pose -2.8 %, profiles/r5q_ttfp_probe.jsonl)
     const bool archived = !truncate || explicit_rk;
     if (abort_mode && archived) return HC_ERROR_INVALID_VALUE;
-    const void *kern = abort_mode ? (const void *)k_track<true, 4, true>
+#ifndef HC_ABORT_GTAB
+#define HC_ABORT_GTAB true
+#endif
+#ifndef HC_ABORT_MINW
+#define HC_ABORT_MINW 4
+#endif
+    const void *kern = abort_mode ? (const void *)k_track<true, HC_ABORT_MINW, HC_ABORT_GTAB>
                        : archived ? (const void *)k_track<false, 5, true, true>
                                   : (const void *)k_track<false, 5, true>;
     // the structure-agnostic twin, enqueued after it: exactly one of the two
     // tracks (EvalTables::lu_struct), the other returns at its first load
-    const void *kern_any = abort_mode ? (const void *)k_track<true, 4, true, false, false>
+    const void *kern_any = abort_mode ? (const void *)k_track<true, HC_ABORT_MINW, HC_ABORT_GTAB, false, false>
                            : archived ? (const void *)k_track<false, 5, true, true, false>
                                       : (const void *)k_track<false, 5, true, false, false>;
     const int grid = grid_for((int)((paths + 1) / 2), kern);
@@ -1964,7 +1985,7 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.4 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+    return "hc_trifocal gfx950 v10.5 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
            "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
            "column groups by structural class (never-fillable groups untested, always-live groups unconditional), "
            "pivot search narrowed to the candidate rows' DPP group "
