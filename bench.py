@@ -99,6 +99,9 @@ def parse():
                     help="samples per GPU of the early-abort (config 3/4) time-to-first-good-pose run; 0 disables")
     ap.add_argument("--abort-repeats", type=int, default=12,
                     help="runs per abort semantics in the early-abort leg (median, min and max reported)")
+    ap.add_argument("--abort-seeds", type=int, default=8,
+                    help="early-abort leg: also srand(1..K) draws of the same data (first pose across hypotheses)")
+    ap.add_argument("--abort-seed-repeats", type=int, default=3)
     ap.add_argument("--abort-chunk", type=int, default=125,
                     help="samples per launch in the early-abort run (the cross-GPU flag is reduced between launches)")
     ap.add_argument("--noisy-trials", type=int, default=30,
@@ -391,41 +394,49 @@ def main():
                                              if peer.ptr is not None else
                                              f"RCCL all_reduce at chunk boundaries only ({peer.error})")
         n_chunks = len(sharding.chunks(cnt, args.abort_chunk))
+
+        def abort_run(inflight):
+            """One config-3 run of this rank's shard: (first-pose seconds, min over
+            ranks; wall seconds, max over ranks; paths tracked, summed over ranks;
+            this rank's [self found, paths tracked, found byte] of every rank)."""
+            tr.reset_tracks(ra)
+            torch.cuda.synchronize(dev)
+            if peer is not None:
+                peer.arm(stream)          # zeroed by its owner, then a barrier
+            elif world > 1:
+                dist.barrier()
+            w0 = time.perf_counter()
+            tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream, inflight_stop=inflight,
+                                    peer_found=peer if peer is not None and peer.ptr is not None else None,
+                                    max_count=sharding.max_shard(Sa * world, world))
+            torch.cuda.synchronize(dev)
+            w = time.perf_counter() - w0
+            hz = tr.read_timestamps(wss[0])[2]
+            stamps = [tr.read_timestamps(x)[:2] for x in wss[:n_chunks]]
+            f = sharding.first_found_seconds(stamps, hz)
+            n_tr = int((ra.stats[:, 0] > 0).sum().item())
+            # per rank: did it find a pose itself (a found stamp in one of its own
+            # launches), how many of its shard's paths it tracked, and the found
+            # byte it ended with (its own find, the peer flag or the chunk reduction)
+            self_found = any(fs for _, fs in stamps)
+            pr = gather_floats([1.0 if self_found else 0.0, float(n_tr), float(bool(ra.found.item()))], dev, world)
+            if world > 1:
+                v = torch.tensor([f if f >= 0 else 1e30, -w, -float(n_tr)], dtype=torch.float64, device=dev)
+                dist.all_reduce(v, op=dist.ReduceOp.MIN)
+                f, w = float(v[0].item()), -float(v[1].item())
+                f = -1.0 if f >= 1e29 else f
+                nt = torch.tensor([n_tr], dtype=torch.int64, device=dev)
+                dist.all_reduce(nt)
+                n_tr = int(nt.item())
+            return f, w, n_tr, pr
+
         for inflight in (False, True):
             ttfp, wall, tracked = [], [], []
             found_runs, per_rank_runs = [], []
             for _ in range(args.abort_repeats):
-                tr.reset_tracks(ra)
-                torch.cuda.synchronize(dev)
-                if peer is not None:
-                    peer.arm(stream)          # zeroed by its owner, then a barrier
-                elif world > 1:
-                    dist.barrier()
-                w0 = time.perf_counter()
-                tr.launch_abort_chunked(ta, da, ra, args.abort_chunk, wss, stream=stream, inflight_stop=inflight,
-                                        peer_found=peer if peer is not None and peer.ptr is not None else None,
-                                        max_count=sharding.max_shard(Sa * world, world))
-                torch.cuda.synchronize(dev)
-                w = time.perf_counter() - w0
-                hz = tr.read_timestamps(wss[0])[2]
-                stamps = [tr.read_timestamps(x)[:2] for x in wss[:n_chunks]]
-                f = sharding.first_found_seconds(stamps, hz)
-                n_tr = int((ra.stats[:, 0] > 0).sum().item())
-                # per rank: did it find a pose itself (a found stamp in one of its own
-                # launches), how many of its shard's paths it tracked, and the found
-                # byte it ended with (its own find, the peer flag or the chunk reduction)
-                self_found = any(fs for _, fs in stamps)
-                per_rank_runs.append(gather_floats([1.0 if self_found else 0.0, float(n_tr),
-                                                    float(bool(ra.found.item()))], dev, world))
+                f, w, n_tr, pr = abort_run(inflight)
+                per_rank_runs.append(pr)
                 found_runs.append(bool(ra.found.item()))
-                if world > 1:
-                    v = torch.tensor([f if f >= 0 else 1e30, -w, -float(n_tr)], dtype=torch.float64, device=dev)
-                    dist.all_reduce(v, op=dist.ReduceOp.MIN)
-                    f, w = float(v[0].item()), -float(v[1].item())
-                    f = -1.0 if f >= 1e29 else f
-                    nt = torch.tensor([n_tr], dtype=torch.int64, device=dev)
-                    dist.all_reduce(nt)
-                    n_tr = int(nt.item())
                 ttfp.append(f)
                 wall.append(w)
                 tracked.append(n_tr)
@@ -447,6 +458,34 @@ def main():
                 "per_rank": ranks,
                 "peer_stop_observed": any(r_["peer_stopped_runs"] > 0 for r_ in ranks),
                 "peer_stop_mid_launch_observed": any(r_["peer_stopped_mid_launch_runs"] > 0 for r_ in ranks)}
+        # the first pose over other RANSAC draws of the same data (VERDICT r5:
+        # one seed measures one path's latency): srand(1..K), reference semantics,
+        # the median of a few runs each and where the first passing sample sits
+        seeds = []
+        for sd in range(1, args.abort_seeds + 1):
+            ts_all, ds_all, _ = prepare_target_params(problem, data, seed=sd, num_samples=Sa * world, num_gpus=world)
+            ta.copy_(torch.from_numpy(ts_all[off:off + cnt]))
+            da.copy_(torch.from_numpy(ds_all[off:off + cnt]))
+            fs = [abort_run(False)[0] for _ in range(args.abort_seed_repeats)]
+            bi = ra.batch_index.cpu().numpy()
+            hit = np.nonzero(bi >= 0)[0]
+            first = float(off + hit[0] // 312) if len(hit) else 1e30
+            if world > 1:
+                v = torch.tensor([first], dtype=torch.float64, device=dev)
+                dist.all_reduce(v, op=dist.ReduceOp.MIN)
+                first = float(v.item())
+            ok = [f for f in fs if f >= 0]
+            seeds.append({"srand": sd, "first_passing_sample": None if first >= 1e29 else int(first),
+                          "time_to_first_good_pose_ms": round(float(np.median(ok)) * 1e3, 3) if ok else None})
+        if seeds:
+            got = [x["time_to_first_good_pose_ms"] for x in seeds if x["time_to_first_good_pose_ms"] is not None]
+            abort_info["across_seeds"] = {
+                "runs_per_seed": args.abort_seed_repeats, "seeds": seeds,
+                "found_seeds": len(got), "median_ms": round(float(np.median(got)), 3) if got else None,
+                "quartiles_ms": [round(float(np.percentile(got, 25)), 3), round(float(np.percentile(got, 75)), 3)]
+                if got else None,
+                "note": "dataset 000, samples srand(1..K) instead of srand(0); reference semantics; the time "
+                        "follows where the first passing hypothesis sits in the sample order"}
         if peer is not None:
             peer.close()
         abort_info["note"] = ("device clock (s_memrealtime, rate from hipDeviceAttributeWallClockRate) from the "
@@ -582,7 +621,7 @@ def main():
             line["noisy_pose"] = noisy_info
         if abort_info is not None:
             line["early_abort"] = abort_info
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:   # the CPU baseline is timed at N = 1 only
             line["cpu_baseline"] = cpu_baseline(problem, data, args.cpu_samples, args.cpu_samples_4t,
                                                 args.cpu_samples_ref, value)
         print(json.dumps(line), flush=True)
