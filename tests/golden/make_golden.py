@@ -17,8 +17,11 @@ outputs pin the oracle so later rounds (and the GPU box, which has no
                         (noise seed 20250215, the bench's first trial), samples srand(0), 100
                         samples: per-path flags / counts / hashes, the scoring of every
                         converged path, and the maximal-support selection with its GT residuals
+  gpuhc_ds{010,050,099}_N100_seed0.npz  config 2 on held-out synthcurves datasets (round 6):
+                        flags / counts / hashes, scoring, the maximal-support pose vs that dataset's GT
+  cli_rounds_counts.npz the solution counts of `magmaHC-main -t 4`'s rounds 0..3 (dataset ti, srand(ti))
 
-Run:  python tests/golden/make_golden.py [--only pose|noisy]   (takes ~1-2 min on 8 cores)
+Run:  python tests/golden/make_golden.py [--only pose|noisy|heldout_golden|cli_rounds|...]   (takes ~1-2 min on 8 cores)
 """
 import os
 import sys
@@ -142,6 +145,21 @@ def heldout_golden(ss, sp, U, K):
               "candidates", sel["num_candidates"], "residuals", res, ok)
 
 
+def cli_rounds_fixture(ss, sp, U):
+    """The CLI's rounds ti = 0..3 (`magmaHC-main -t 4`, cmd/magmaHC-main.cpp:38-48):
+    round ti reads Triplet_Edgels_<ti> and draws its samples with srand(ti)
+    (GPU_HC_Solver.cpp:252-306); 100 samples each: the solution counts the CLI
+    writes to GPU_Sols_Statistics.txt, one row per round."""
+    counts = []
+    for ti in range(4):
+        loc, tan = O.read_edgels(os.path.join(RANS, "Triplet_Edgels", f"Triplet_Edgels_{ti:03d}.txt"))
+        tgt, dif, _ = O.prepare_target_params(ti, [100], loc, tan, sp)
+        tr, conv, inf, _ = O.gpuhc_track(ss, sp, tgt, dif, U)
+        counts.append(O.count_solutions(tr, conv, inf))
+        print(f"round {ti}: counts", counts[-1])
+    np.savez_compressed(os.path.join(HERE, "cli_rounds_counts.npz"), counts=np.array(counts, np.int64))
+
+
 def ph_codeopt_fixture(ss, sp, U, tgt, dif, explicit_rk=False):
     """Config 2 through the archived ..._PH_CodeOpt semantics (no depth-sign
     truncation; the archived kernel is ..._TrunPaths without :148-155), or with
@@ -198,6 +216,9 @@ def main():
         return
     if only == "heldout_golden":
         heldout_golden(ss, sp, U, K)
+        return
+    if only == "cli_rounds":
+        cli_rounds_fixture(ss, sp, U)
         return
     if only == "pose":
         tr, conv, inf, st = O.gpuhc_track(ss, sp, tgt, dif, U)

@@ -460,7 +460,8 @@ def test_cli_four_rounds(tmp_path):
     """`magmaHC-main -t 4` (TEST_RANSAC_TIMES = 4; cmd/magmaHC-main.cpp:38-48):
     round ti reads Triplet_Edgels_<ti> and GT_Poses*_<ti> and draws its samples
     with srand(ti) (GPU_HC_Solver.cpp:252-306).  Every round writes its timing,
-    solution statistics and pose line; round 0 equals the golden counts."""
+    solution statistics and pose line; every round's counts equal the oracle's
+    (tests/golden/cli_rounds_counts.npz)."""
     import shutil
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -476,6 +477,9 @@ def test_cli_four_rounds(tmp_path):
     assert len(stats) == 4 and all(int(r[0]) > 0 for r in stats)
     g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
     assert [int(v) for v in stats[0]] == [int(v) for v in g["counts"]]
+    # every round's counts equal the oracle's run of that round's dataset and draw
+    rounds = np.load(os.path.join(GOLDEN, "cli_rounds_counts.npz"))["counts"]
+    assert [[int(v) for v in r[:3]] for r in stats] == rounds.tolist()
     assert len(open(os.path.join(od, "GPU_Pose_Results.txt")).read().splitlines()) == 4
     assert "Running 4 rounds" in out.stdout
 
