@@ -57,6 +57,17 @@ for mode in ("sliced", "unsliced"):
                  "pairing_efficiency": round(float(ps.sum()) / (2 * max(1, ws.sum())), 4),
                  "utilisation_vs_steady": round(float(rel.mean()), 4),
                  "rate_2pct_bins_rel_steady": [round(float(v), 3) for v in rel]}
+    # per path (HC_DIAG_TIMES writes the first dequeue and the finish stamp,
+    # s_memrealtime low 32 bits, into the stats record): when the paths finish
+    # and which ones finish last
+    st = r.stats.cpu().numpy().astype(np.int64)
+    t_deq = (st[:, 2] - (t0 & 0xFFFFFFFF)) % (1 << 32)
+    t_fin = (st[:, 3] - (t0 & 0xFFFFFFFF)) % (1 << 32)
+    order = np.argsort(t_fin)
+    out[mode]["finish_quantiles_ms"] = {q: round(float(np.percentile(t_fin, q)) * 1e-5, 3) for q in (50, 90, 95, 99, 100)}
+    out[mode]["last_paths"] = [{"path": int(b), "steps": int(st[b, 0]), "corrections": int(st[b, 1]),
+                                "first_start_ms": round(float(t_deq[b]) * 1e-5, 3),
+                                "finish_ms": round(float(t_fin[b]) * 1e-5, 3)} for b in order[-12:]]
     print(json.dumps({k: v for k, v in out[mode].items() if k != "rate_2pct_bins_rel_steady"}), flush=True)
 with open(sys.argv[1], "w") as f:
     json.dump(out, f, indent=1)
