@@ -1098,7 +1098,13 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
                     done = (double)t0 > 0.95 && check;
                 }
                 bool suspend = false;
-                if (!ABORT && !done && a.slice_q > 0 && piece >= a.slice_q) {
+#ifndef HC_SLICE_HOLD
+#define HC_SLICE_HOLD 0
+#endif
+                // HC_SLICE_HOLD (A/B, 0 = off): a path that has run this many
+                // steps keeps its slot to the end (the likely 81-step paths)
+                if (!ABORT && !done && a.slice_q > 0 && piece >= a.slice_q &&
+                    (HC_SLICE_HOLD == 0 || stepidx < HC_SLICE_HOLD)) {
                     // time slice used up: suspend for a new path (its ticket
                     // claimed here), else swap with a suspended path, else
                     // keep running
