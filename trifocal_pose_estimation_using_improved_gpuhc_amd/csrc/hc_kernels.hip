@@ -1226,7 +1226,17 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 #else
             const int si = (ph == PH_STAGE) ? stepidx : (1 << 20);
             const int m = min(__builtin_amdgcn_readlane(si, 0), __builtin_amdgcn_readlane(si, 32));
-            const int q4 = (int)((long long)m * 4 / (a.max_steps + 1));
+            int q4 = (int)((long long)m * 4 / (a.max_steps + 1));
+#ifndef HC_PRIO_LAS
+#define HC_PRIO_LAS 1
+#endif
+            // A/B (HC_PRIO_LAS): 0 = one priority for all, -1 = most attained
+            // service first (a boost for the long paths)
+#ifdef HC_PRIO_STEPW
+            q4 = min(m / HC_PRIO_STEPW, 3);
+#endif
+            if (HC_PRIO_LAS == 0) q4 = 3;
+            if (HC_PRIO_LAS < 0) q4 = 3 - q4;
 #endif
             if (q4 <= 0) __builtin_amdgcn_s_setprio(3);
             else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
