@@ -20,6 +20,13 @@ extern "C" {
 #define HC_RING_TEST_MIN_TICKS 4096
 void hc_trifocal_set_ring_test(int delay_ticks);
 
+/* Which instantiation a tracking launch (hc_trifocal_2op1p_30x30_track) runs:
+   0 (the default) the latency-mode kernel when the launch fills at most half
+   of the device's path slots, the throughput kernel otherwise; 1 always the
+   latency-mode kernel; -1 never.  The results are the same bit for bit; only
+   the speed differs.  Read at launch time. */
+void hc_trifocal_set_small_launch(int mode);
+
 /* The end-of-launch ring check of a sliced launch (k_ring_check) on ring
    counters set by hand: head, tail and avail are written into the workspace's
    time-slicing area (workspace_bytes must cover the workspace and the ring

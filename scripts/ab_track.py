@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of tracker library builds (development tool, GPU only).
 
-    python scripts/ab_track.py NAME=path/to/lib.so [NAME=...] [--rounds 2] [--samples 100]
+    python scripts/ab_track.py NAME=path/to/lib.so [NAME=...] [--rounds 2] [--samples 100] [--sizes 2,8,32]
 
 Runs each build in its own process (HC_TRIFOCAL_LIB), rounds interleaved
 (A B A B ...): config-2 launches timed with HIP events on the launch stream
@@ -17,7 +17,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(samples):
+def child(samples, sizes=()):
     sys.path.insert(0, ROOT)
     import numpy as np
     import torch
@@ -39,7 +39,7 @@ def child(samples):
     tgt, dif, _ = prepare_target_params(problem, load_ransac_data(0), 0, max(100, samples))
     tr = DeviceTracker(problem, dev)
     out = {}
-    for n, reps in ((samples, 7), (1, 5)):
+    for n, reps in ((samples, 7), (1, 5)) + tuple((k, 5) for k in sizes):
         r = tr.allocate(n)
         t, d = torch.from_numpy(tgt[:n]).to(dev), torch.from_numpy(dif[:n]).to(dev)
         s = torch.cuda.current_stream(dev)
@@ -67,11 +67,12 @@ def main():
     args = [a for a in sys.argv[1:] if "=" in a]
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 2
     samples = int(sys.argv[sys.argv.index("--samples") + 1]) if "--samples" in sys.argv else 100
+    sizes = sys.argv[sys.argv.index("--sizes") + 1] if "--sizes" in sys.argv else ""
     builds = [a.split("=", 1) for a in args]
     for rnd in range(rounds):
         for name, lib in builds:
             env = dict(os.environ, HC_TRIFOCAL_LIB=os.path.abspath(lib))
-            p = subprocess.run([sys.executable, __file__, "--child", str(samples)], env=env, capture_output=True,
+            p = subprocess.run([sys.executable, __file__, "--child", str(samples), "--sizes", sizes], env=env, capture_output=True,
                                text=True, timeout=300)
             if p.returncode != 0:
                 print(json.dumps({"build": name, "round": rnd, "error": p.stderr[-2000:]}), flush=True)
@@ -82,6 +83,7 @@ def main():
 
 if __name__ == "__main__":
     if "--child" in sys.argv:
-        child(int(sys.argv[sys.argv.index("--child") + 1]))
+        sz = sys.argv[sys.argv.index("--sizes") + 1] if "--sizes" in sys.argv else ""
+        child(int(sys.argv[sys.argv.index("--child") + 1]), tuple(int(k) for k in sz.split(",") if k))
     else:
         main()

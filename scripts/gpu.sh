@@ -18,7 +18,7 @@
 #   phases    per-phase cycles of the HC_DIAG_PHASES build (scripts/diag_phases.py)
 #   stress    time slicing under concurrent streams (scripts/slice_stress.py: 4 cold, 4 warm, 8 cold)
 #   validate  tests,luwork,bench,profile,datasets
-# Extra environment: BENCH_ARGS (bench step), AB_ROUNDS (ab step, default 3), TTFP_ARGS (ttfp_ab step,
+# Extra environment: BENCH_ARGS (bench step), AB_ROUNDS (ab step, default 3), AB_ARGS (more ab_track.py options), TTFP_ARGS (ttfp_ab step,
 # e.g. "--dataset 10").
 export TMPDIR=/tmp
 cd ${GRAFT_REPO_ROOT:-$(dirname "$0")/..}
@@ -69,7 +69,7 @@ for step in ${STEPS//,/ }; do
       args=""; last=""
       for kv in "$@"; do args="$args ${kv%%=*}=$P/${kv#*=}"; last=$P/${kv#*=}; done
       HC_TRIFOCAL_LIB=$last run ab_parity 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu --timeout 200 --timeout-method thread -k "not cli" > $O/${T}_parity.log 2>&1; rc=$?; tail -3 $O/${T}_parity.log
-      [ $rc -eq 0 ] && { run ab 900 python -u scripts/ab_track.py $args --rounds ${AB_ROUNDS:-3} > $O/${T}_ab.jsonl; rc=$?; cat $O/${T}_ab.jsonl; } ;;
+      [ $rc -eq 0 ] && { run ab 900 python -u scripts/ab_track.py $args --rounds ${AB_ROUNDS:-3} $AB_ARGS > $O/${T}_ab.jsonl; rc=$?; cat $O/${T}_ab.jsonl; } ;;
     ttfp_ab)
       rc=0
       for kv in "$@"; do

@@ -4,6 +4,7 @@ Bar: identical values -- the kernel and the oracle implement the sam
 op-level spec, so every float must match exactly, treating +0 == -0 and
 NaN == NaN; converged / infinity flags and step / correction counts identical.
 """
+import contextlib
 import ctypes
 import os
 
@@ -15,6 +16,21 @@ from conftest import same
 pytestmark = pytest.mark.gpu
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# Tracking launches run the latency-mode kernel (k_track_small) when they fill
+# at most half of the path slots (N <= 16 samples), the throughput kernel
+# (k_track) otherwise; the tests below run each size through both
+# (hc_trifocal_set_small_launch: 0 by size, 1 always small, -1 never).
+KERNEL_BY_SIZE, SMALL_ALWAYS, SMALL_NEVER = 0, 1, -1
+
+
+@contextlib.contextmanager
+def small_launch(L, mode):
+    L.hc_trifocal_set_small_launch(mode)
+    try:
+        yield
+    finally:
+        L.hc_trifocal_set_small_launch(KERNEL_BY_SIZE)
 
 
 def _jacobians_from_path(problem, oracle, tgt, dif, n=64, seed=1):
@@ -124,11 +140,13 @@ def test_cgesv_extreme_scales(problem, oracle, samples100):
         assert same(xg[i], xr).all(), f"extreme-scale LU mismatch on system {i}"
 
 
-def test_tracker_matches_oracle_small(problem, oracle, samples100, tracker):
+@pytest.mark.parametrize("mode", [KERNEL_BY_SIZE, SMALL_NEVER], ids=["latency_kernel", "throughput_kernel"])
+def test_tracker_matches_oracle_small(problem, oracle, samples100, tracker, mode):
     """Full GPU-HC tracking of 2 samples (624 paths) vs the oracle, value for value."""
     tgt, dif, _ = samples100
     N = 2
-    r = tracker.track(tgt[:N], dif[:N]).host()
+    with small_launch(tracker.L, mode):
+        r = tracker.track(tgt[:N], dif[:N]).host()
     tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, tgt[:N], dif[:N],
                                            problem.unified_index)
     assert (r["converge"] == conv).all()
@@ -141,7 +159,8 @@ def test_tracker_matches_oracle_small(problem, oracle, samples100, tracker):
     assert (r["tracks"][:, 30, 0] == 1.0).all()
 
 
-def test_tracker_dense_resolve_matches_oracle(problem, oracle, samples100, tracker):
+@pytest.mark.parametrize("mode", [KERNEL_BY_SIZE, SMALL_NEVER], ids=["latency_kernel", "throughput_kernel"])
+def test_tracker_dense_resolve_matches_oracle(problem, oracle, samples100, tracker, mode):
     """The tracker's dense re-solve (hc_lu.hpp lu_solve<true>, taken when a
     Jacobian entry reaches 2^64 or a pivot leaves the fast-reciprocal range):
     config 2 never takes it (profiles/r3e_lu_work.json), so this run forces it.
@@ -158,7 +177,8 @@ def test_tracker_dense_resolve_matches_oracle(problem, oracle, samples100, track
     T = np.stack(T)
     D = (T - problem.start_params[None]).astype(np.float32)   # prepare_target_params' diff
     assert np.array_equal(D[0], dif[0])
-    r = tracker.track(T, D).host()
+    with small_launch(tracker.L, mode):
+        r = tracker.track(T, D).host()
     tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, T, D, problem.unified_index)
     assert (r["converge"] == conv).all() and (r["infinity"] == inf).all()
     assert (r["stats"]["steps"] == st["steps"]).all()
@@ -190,14 +210,16 @@ def test_tracker_dense_resolve_abort_mode(problem, oracle, samples100, tracker):
     assert inf[:624].sum() > 600
 
 
-def test_tracker_matches_golden_N100(problem, samples100, tracker):
+@pytest.mark.parametrize("mode", [KERNEL_BY_SIZE, SMALL_ALWAYS], ids=["throughput_kernel", "latency_kernel"])
+def test_tracker_matches_golden_N100(problem, samples100, tracker, mode):
     """Config 2 (100 samples, abort off): every flag / count / track hash equals the committed golden run."""
     import sys
     sys.path.insert(0, GOLDEN)
     from make_golden import track_hash
     g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
     tgt, dif, _ = samples100
-    r = tracker.track(tgt, dif).host()
+    with small_launch(tracker.L, mode):
+        r = tracker.track(tgt, dif).host()
     assert (r["converge"] == g["conv"]).all()
     assert (r["infinity"] == g["inf"]).all()
     assert (r["stats"]["steps"] == g["steps"]).all()
@@ -616,7 +638,8 @@ def _outside_lu_structure(dx):
     return [r for r in range(30) if pat[r] & ~int(L.hc_lu_struct_pattern(r))]
 
 
-def test_tracker_row_permuted_structure_matches_oracle(problem, oracle, samples100, ransac0):
+@pytest.mark.parametrize("mode", [KERNEL_BY_SIZE, SMALL_NEVER], ids=["latency_kernel", "throughput_kernel"])
+def test_tracker_row_permuted_structure_matches_oracle(problem, oracle, samples100, ransac0, mode):
     """Any table the reference kernel takes is tracked.  A
     row-permuted system (valid and equivalent) has a dH/dx structure outside
     the one the specialised LU compiles in; k_prep_tables routes it to the
@@ -639,7 +662,8 @@ def test_tracker_row_permuted_structure_matches_oracle(problem, oracle, samples1
         tr = DeviceTracker(dataclasses.replace(problem, dHdx_index=dx, dHdt_index=dt), torch.device("cuda:0"))
         tr.set_ransac_data(ransac0)
         for truncate in (True, False):
-            r = tr.track(tgt[:N], dif[:N], truncate=truncate).host()
+            with small_launch(tr.L, mode):
+                r = tr.track(tgt[:N], dif[:N], truncate=truncate).host()
             tr.workspace_status()
             o_tr, conv, inf, st = oracle.gpuhc_track(problem.start_sols, problem.start_params, tgt[:N], dif[:N], U,
                                                      oracle.settings(truncate=truncate))

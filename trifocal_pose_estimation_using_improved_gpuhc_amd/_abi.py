@@ -94,6 +94,9 @@ def lib() -> C.CDLL:
             raise HCError(f"{LIB_PATH}: ABI {L.hc_trifocal_abi_version()}, this binding expects {ABI_VERSION}")
         L.hc_trifocal_set_ring_test.restype = None
         L.hc_trifocal_set_ring_test.argtypes = [C.c_int]
+        if hasattr(L, "hc_trifocal_set_small_launch"):   # (test hook, round 6)
+            L.hc_trifocal_set_small_launch.restype = None
+            L.hc_trifocal_set_small_launch.argtypes = [C.c_int]
         if hasattr(L, "hc_trifocal_ring_check_test"):   # (test hook, round 6)
             L.hc_trifocal_ring_check_test.restype = C.c_int
             L.hc_trifocal_ring_check_test.argtypes = [C.c_void_p, C.c_size_t, C.c_uint, C.c_uint, C.c_uint, C.c_void_p]
@@ -178,7 +181,7 @@ DECLARED_SYMBOLS = (
     "hc_trifocal_2op1p_30x30_track_ph_codeopt", "hc_trifocal_2op1p_30x30_track_ph",
     "hc_trifocal_workspace_status", "hc_trifocal_read_timings", "hc_trifocal_read_timestamps", "hc_cgesv_30x30_batched", "hc_trifocal_eval_batched", "hc_trifocal_version",
     "hc_last_error_string", "hc_trifocal_abi_version", "hc_trifocal_set_ring_test",
-    "hc_trifocal_ring_check_test",
+    "hc_trifocal_ring_check_test", "hc_trifocal_set_small_launch",
     "hc_lu_struct_pattern", "hc_lu_group_class", "hc_lu_candidates", "hc_lu_search_span",
     "hc_shared_flag_create", "hc_shared_flag_open", "hc_shared_flag_reset", "hc_shared_flag_close",
     "hc_shared_flag_memory_kind",

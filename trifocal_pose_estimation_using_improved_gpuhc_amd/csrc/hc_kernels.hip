@@ -874,603 +874,25 @@ typedef uint32_t T_hxd_t[HX_NSLOT / 2][32];
 template <bool ABORT, int MINW, bool GTAB, bool ARCH = false, bool LUS = true>
 __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
     // LU (hc_lu.hpp): the abort kernel's time to the first pose is a lone
-    // path's latency, so it runs the latency mode (no exec region for the pivot
-    // row; profiles/r5n_ttfp.jsonl: -2.4 %); the tracking kernels the throughput one
+    // path's latency, so it runs the latency mode (one LDS round trip per pivot
+    // step, in batches of HC_LU_LATB_COLS columns); the tracking kernel the
+    // throughput mode (profiles/r6x_ab_track_latency_lu.jsonl: the latency mode
+    // is 9 % slower per config-2 launch there)
     constexpr int LUCH = LU_CHUNK;
     constexpr int LULAT = ABORT ? HC_LU_LATB_COLS : 0;
-    constexpr bool LUSTRUCT = LUS;
-    constexpr int TAB_BYTES =
-        GTAB ? 16 : (int)(sizeof(uint2) * HT_TERMS * 32 + sizeof(uint32_t) * HX_SLOT_CAP * 32 + sizeof(T_hxd_t));
-    __shared__ __attribute__((aligned(16))) char s_tab[TAB_BYTES];
-    __shared__ cf s_sp[NPP];
-    __shared__ SlotLDS s_slot[2 * WAVES_PER_WG];
-    Workspace *ws = a.ws;
-    const EvalTables *T = &ws->tab;
-    if (ws->status != 0u) return;
-    if ((T->lu_struct == 1u) != LUSTRUCT) return;   // the other instantiation tracks this table
-    // time slicing: this launch's ring epoch (bumped by k_prep_tables)
-    const unsigned epoch = (!ABORT && a.slice_q > 0) ? ld_rlx(&a.rq[RQ_EPOCH]) : 0u;
-    const uint2 *s_ht = GTAB ? T->ht : reinterpret_cast<const uint2 *>(s_tab);
-    const uint32_t *s_hx = GTAB ? T->hx : reinterpret_cast<const uint32_t *>(s_ht + HT_TERMS * 32);
-    const uint32_t *s_hxd = GTAB ? &T->hxd[0][0] : s_hx + HX_SLOT_CAP * 32;
-    if constexpr (!GTAB) {
-        uint2 *t_ht = reinterpret_cast<uint2 *>(s_tab);
-        uint32_t *t_hx = reinterpret_cast<uint32_t *>(t_ht + HT_TERMS * 32), *t_hxd = t_hx + HX_SLOT_CAP * 32;
-        for (int i = threadIdx.x; i < HX_SLOT_CAP * 32; i += WG_THREADS) t_hx[i] = T->hx[i];   // padded table
-        for (int i = threadIdx.x; i < HT_TERMS * 32; i += WG_THREADS) t_ht[i] = T->ht[i];
-        for (int i = threadIdx.x; i < HX_NSLOT / 2 * 32; i += WG_THREADS) t_hxd[i] = (&T->hxd[0][0])[i];
-    }
-    if (threadIdx.x < NPP) s_sp[threadIdx.x] = a.start_params[threadIdx.x];
-    {
-        float *z = reinterpret_cast<float *>(s_slot);
-        for (int i = threadIdx.x; i < (int)(sizeof(s_slot) / 4); i += WG_THREADS) z[i] = 0.0f;
-    }
-    __syncthreads();
-    if (ABORT && threadIdx.x == 0) atomicCAS(&ws->t_start, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    const int lane = lane_id();
-    const int r = lane & 31, hb = lane & 32;
-    const int wid = threadIdx.x / WAVE;
-    SlotLDS &S = s_slot[wid * 2 + (hb >> 5)];
-    if (r == 30) S.x[30] = cmk(1.0f, 0.0f);
-    if (r == 0) S.st.pre_smp = -2;   // no prefix tables yet
-    // per-row constants (gather map, structural pattern) live in LDS and are
-    // re-read every stage: held in VGPRs across the loop they spill (abort mode)
-    __shared__ uint32_t s_rowc[GM_WORDS + 1][32];   // [0..14] gather map (hc_eval.hpp), [15] structural pattern
-    if (threadIdx.x < 32) {
-        for (int q = 0; q < GM_WORDS; q++) s_rowc[q][threadIdx.x] = T->gm[q][threadIdx.x];
-        s_rowc[GM_WORDS][threadIdx.x] = T->pat[threadIdx.x];
-    }
-    __syncthreads();
-    const bool rl = r < NV;
-    wave_lds_sync();
+#include "hc_track_body.inc"
+}
 
-    // per-slot state (uniform within a half)
-    int ph = PH_DEQ, b = -1, smp_loaded = -1;
-    int qpos = 0;   // queue position of the slot's path (issue priority)
-    unsigned found_seen = 0u;   // abort mode: the found flag as of the last stage
-#ifdef HC_DIAG_TIMES
-    int diag_t0 = 0;
-    const unsigned long long diag_w0 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0) atomicMin(&g_diag_span[0], diag_w0);
-#endif
-    int s = 0, stepidx = 0, coef = 1, succ = 0, nsteps = 0, ncorr = 0;
-    int piece = 0;   // steps since the path (re)started on this slot (time slicing)
-    float t0 = 0.0f, t_step = 0.0f, dt = 0.01f, h2 = 0.0f, scale = 0.0f;
-    bool end_zone = false, check = true, isSucc = false, isInf = false;
-    cf x = cmk(0.0f, 0.0f), xl = x, sols = x;
-
-#ifdef HC_DIAG_PHASES
-    uint64_t dg[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    uint64_t dt_ = __builtin_amdgcn_s_memtime(), dt0_ = dt_;
-#define HC_DIAG_MARK(k) do { const uint64_t n_ = __builtin_amdgcn_s_memtime(); dg[k] += n_ - dt_; dt_ = n_; } while (0)
-#else
-#define HC_DIAG_MARK(k) do { } while (0)
-#endif
-    for (;;) {
-        HC_DIAG_MARK(6);
-        HC_ISA_MARK("ctl_slots");
-        // ---------------- resolve slot phases until every slot is at a stage or idle
-        // next dequeue (time slicing): -1 normal, -2 swap with a suspended path,
-        // >= 0 a new-path ticket the suspension claimed (set and used within this phase)
-        int deq_hint = -1;
-        for (;;) {
-            if (ph == PH_FINISH) {                                            // :282-286
-                const bool conv = ((double)t0 >= 1.0 || (1.0 - (double)t0 <= 0.0000001));
-                cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
-                if (rl) dtrack[r] = x;
-                int in21 = 0, in31 = 0;
-                if (ABORT && conv) {                                          // TrunRANSAC.cu:312-322
-                    if (rl) S.x[r] = x;
-                    wave_lds_sync();
-                    const unsigned long long im = __ballot(r >= 18 && rl && (double)__builtin_fabsf(x.y) < 1e-5);
-                    if (((unsigned)(im >> hb) & 0x3FFC0000u) == 0x3FFC0000u) {   // eval.cuh:46-53
-                        const int2 c = score_half(S.x, a.edgels, a.num_edgels, a.K, r);
-                        in21 = c.x;
-                        in31 = c.y;
-                        const float r21 = (float)in21 / (float)a.num_edgels, r31 = (float)in31 / (float)a.num_edgels;
-                        if ((double)r21 >= 0.90 && (double)r31 >= 0.90 && r == 0) {   // eval.cuh:241-246
-                            __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            a.found_flag[0] = 1;
-                            // the other GPUs' launches poll this (system scope: written
-                            // through to the owner's memory over xGMI)
-                            if (a.peer_found)
-                                __hip_atomic_store(a.peer_found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                            a.batch_index[b] = b;
-                            atomicCAS(&ws->t_found, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
-                        }
-                    }
-                }
-                if (r == 0) {
-                    a.conv[b] = conv ? 1 : 0;
-                    a.inf[b] = isInf ? 1 : 0;
-#ifdef HC_DIAG_TIMES
-                    // diagnostic build: dequeue / finish device timestamps (s_memrealtime) of each path
-                    in21 = diag_t0;
-                    in31 = (int)__builtin_amdgcn_s_memrealtime();
-#endif
-                    if (a.stats) a.stats[b] = hcPathStats{nsteps, ncorr, in21, in31};
-                }
-                ph = PH_DEQ;
-            }
-            if (ph == PH_DEQ) {
-                int nb = 0, rb = -1;   // new-path ticket; else a suspended path id (time slicing)
-                if (r == 0) {
-                    if (!ABORT && deq_hint >= 0) {
-                        nb = deq_hint;                       // claimed by the suspension
-                    } else if (!ABORT && deq_hint == -2) {
-                        nb = a.num_paths;                    // swap: the oldest suspended path
-                        rb = ring_pop_paired(a.rq, a.ring, a.ring_cap, epoch, ws, a.num_paths, ring_wait_ticks(a.ring_test));
-                    } else {
-                        nb = (ABORT || a.slice_q == 0 || ld_rlx(&ws->queue) < (unsigned)a.num_paths)
-                                 ? (int)atomicAdd(&ws->queue, 1u) : a.num_paths;
-                        if (!ABORT && nb >= a.num_paths && a.slice_q > 0) rb = ring_pop(a.rq, a.ring, a.ring_cap, epoch, ws, a.num_paths, ring_wait_ticks(a.ring_test));
-                    }
-                }
-                deq_hint = -1;
-                nb = bcast_half0(nb);
-                if (!ABORT) rb = bcast_half0(rb);
-                if (!ABORT && rb >= 0) {
-                    // resume a suspended path at its step boundary from its
-                    // suspend block (x in words 0..29, the scalars in 30, 31)
-                    b = rb;
-                    qpos = 0;
-                    smp_loaded = b / NTRK;   // (its target / diff params are read where the prefixes are built)
-                    const unsigned long long *blk = a.susp + (size_t)b * SUSP_WORDS;
-                    x = rl ? ld_cf_rlx(reinterpret_cast<const cf *>(blk + r)) : cmk(0.0f, 0.0f);
-                    xl = x;
-                    sols = x;
-                    const unsigned long long q0 = ld_u64_h(blk + 30), q1 = ld_u64_h(blk + 31);
-                    t0 = __uint_as_float((unsigned)q0);
-                    dt = __uint_as_float((unsigned)(q0 >> 32));
-                    stepidx = (int)((unsigned)q1 & 0xFFFFu);
-                    nsteps = (int)((unsigned)q1 >> 16);
-                    const unsigned w3 = (unsigned)(q1 >> 32);
-                    ncorr = (int)(w3 & 0xFFFFu);
-                    succ = (int)((w3 >> 16) & 0x3FFFu);
-                    end_zone = (w3 >> 30) & 1u; check = (w3 >> 31) & 1u; isSucc = false; isInf = false;
-                    t_step = 0.0f;
-                    piece = 0;
-                    ph = PH_BEGIN;
-                } else if (nb >= a.num_paths) {
-                    ph = PH_IDLE;
-                    b = -1;
-                } else {
-                    b = path_of_queue_pos(nb, a.num_paths, a.ordered);
-                    qpos = nb;
-                    bool skip = false;
-                    if (ABORT) {                                              // TrunRANSAC.cu:152
-                        skip = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
-                        if (!skip && a.peer_found &&
-                            __hip_atomic_load(a.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) {
-                            // another GPU found a pose: stop here too, and let the rest of
-                            // this launch see it without crossing xGMI
-                            skip = true;
-                            __hip_atomic_store(&ws->found, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        }
-                        skip = bcast_half0((int)skip) != 0;
-                        if (skip && r == 0) {
-                            a.conv[b] = 0;
-                            a.inf[b] = 0;
-                            if (a.stats) a.stats[b] = hcPathStats{0, 0, 0, 0};
-                        }
-                    }
-                    if (!skip) {
-                        const int trk = b % NTRK;                            // :67-69
-                        smp_loaded = b / NTRK;
-#ifdef HC_DIAG_TIMES
-                        diag_t0 = (int)__builtin_amdgcn_s_memrealtime();
-#endif
-                        const cf *dtrack = a.track_array ? a.track_array[b] : a.tracks + (size_t)b * (NV + 1);
-                        const cf *dstart = a.start_sols_array ? a.start_sols_array[trk]
-                                                              : a.start_sols + (size_t)trk * (NV + 1);
-                        x = rl ? dtrack[r] : cmk(0.0f, 0.0f);                 // :101-103
-                        sols = rl ? dstart[r] : cmk(0.0f, 0.0f);
-                        xl = x;
-                        t0 = 0.0f; t_step = 0.0f; dt = 0.01f;                 // :80
-                        end_zone = false; check = !ARCH || a.truncate != 0; isSucc = false; isInf = false;
-                        succ = 0; nsteps = 0; ncorr = 0; stepidx = 0; piece = 0;
-                        ph = PH_BEGIN;
-                    }
-                }
-            }
-            if (ABORT && ph == PH_BEGIN && stepidx > 0 && found_seen != 0u) {
-                // inflight_stop: a pose was found, a path in flight stops at its
-                // step boundary and reports like a skipped one (track untouched,
-                // conv = 0).  Without it (the reference's semantics) in-flight
-                // paths run to completion (..._TrunRANSAC.cu:152 only gates the start).
-                if (r == 0) {
-                    a.conv[b] = 0;
-                    a.inf[b] = 0;
-                    if (a.stats) a.stats[b] = hcPathStats{0, 0, 0, 0};
-                }
-                ph = PH_DEQ;
-            }
-            if (ph == PH_BEGIN) {                                             // :138-165
-                bool done = stepidx > a.max_steps;
-                if (!done) done = !((double)t0 < 1.0 && (1.0 - (double)t0 > 0.0000001));
-                if (!done) {
-                    if (!end_zone && (double)__builtin_fabsf(1.0f - t0) <= 0.0500001) end_zone = true;
-                    if (check) {
-                        const unsigned long long pos = __ballot(r < 8 && x.x > 0.0f);
-                        const bool allpos = ((unsigned)(pos >> hb) & 0xFFu) == 0xFFu;
-                        if (t0 > 0.0f) check = !allpos;
-                    }
-                    done = (double)t0 > 0.95 && check;
-                }
-                bool suspend = false;
-#ifndef HC_SLICE_HOLD
-#define HC_SLICE_HOLD 0
-#endif
-                // HC_SLICE_HOLD (A/B, 0 = off): a path that has run this many
-                // steps keeps its slot to the end (the likely 81-step paths)
-                if (!ABORT && !done && a.slice_q > 0 && piece >= a.slice_q &&
-                    (HC_SLICE_HOLD == 0 || stepidx < HC_SLICE_HOLD)) {
-                    // time slice used up: suspend for a new path (its ticket
-                    // claimed here), else swap with a suspended path, else
-                    // keep running
-                    int hint = -1;
-                    if (r == 0) {
-                        if (ld_rlx(&ws->queue) < (unsigned)a.num_paths) {
-                            const int t = (int)atomicAdd(&ws->queue, 1u);
-                            if (t < a.num_paths) hint = t;
-                        }
-                        if (hint < 0) {
-                            // -3: suspended paths wait, but more than one per path
-                            // slot and this slice is shorter than SLICE_QBIG: go on
-                            const int av = ld_i_rlx(reinterpret_cast<const int *>(&a.rq[RQ_AVAIL]));
-                            const int slots = (int)(gridDim.x * (WG_THREADS / WAVE) * 2u);
-                            if (av > 0) hint = (piece >= SLICE_QBIG || av <= slots) ? -2 : -3;
-                        }
-                    }
-                    hint = bcast_half0(hint);
-                    if (hint >= 0 || hint == -2) {
-                        // the whole state in one 256-B block, one store per half:
-                        // lanes 0..29 x, lane 30 (t0, dt), lane 31 the counters
-                        const unsigned w2 = (unsigned)stepidx | ((unsigned)nsteps << 16);
-                        const unsigned w3 = (unsigned)ncorr | ((unsigned)succ << 16) | (end_zone ? 1u << 30 : 0u) |
-                                            (check ? 1u << 31 : 0u);
-                        const unsigned long long word =
-                            rl ? pack2(__float_as_uint(x.x), __float_as_uint(x.y))
-                               : (r == 30 ? pack2(__float_as_uint(t0), __float_as_uint(dt)) : pack2(w2, w3));
-                        st_u64_h(a.susp + (size_t)b * SUSP_WORDS + r, word);
-                        drain_stores();
-                        if (r == 0) ring_push(a.rq, a.ring, a.ring_cap, epoch, b, hint >= 0, ws, a.ring_test);
-                        deq_hint = hint;
-                        suspend = true;
-                    } else if (hint == -1) {
-                        piece = 0;
-                    }
-                }
-                if (!done && !suspend) {
-                    if (end_zone) {
-                        if (dt > __builtin_fabsf(1.0f - t0)) dt = __builtin_fabsf(1.0f - t0);
-                    } else if ((double)dt > __builtin_fabs(0.95 - (double)t0)) {
-                        dt = (float)__builtin_fabs(0.95 - (double)t0);
-                    }
-                    t_step = t0;
-                    h2 = (float)(0.5 * (double)dt);
-                    scale = 0.0f;
-                    coef = 1;
-                    s = 0;
-                    nsteps++;
-                    piece++;
-                }
-                ph = suspend ? PH_DEQ : done ? PH_FINISH : PH_STAGE;
-            }
-            if (__ballot(ph == PH_FINISH || ph == PH_DEQ || ph == PH_BEGIN) == 0ull) break;
-        }
-        if (__ballot(ph == PH_STAGE) == 0ull) break;
-#ifdef HC_DIAG_UTIL
-        {
-            const unsigned long long bs = __ballot(ph == PH_STAGE);
-            if (lane == 0) {
-                const unsigned bin = (unsigned)(__builtin_amdgcn_s_memrealtime() >> 10) & (UTIL_BINS - 1);
-                unsigned long long *u = g_diag_util[blockIdx.x % UTIL_COPIES][bin];
-                atomicAdd(&u[0], (unsigned long long)((bs & 1ull) + ((bs >> 32) & 1ull)));
-                atomicAdd(&u[1], 1ull);
-            }
-        }
-#endif
-        if (ABORT) {
-            // Abort mode: first come, first served.  The queue is sample-major,
-            // so the waves holding the earliest hypotheses get the higher issue
-            // priority (the first sixteenth of the launch's paths at 3, the next
-            // at 2, the next at 1) and whole early hypotheses complete -- and are
-            // scored -- sooner, instead of every hypothesis in flight
-            // progressing at the same rate.  Which paths are tracked, and their
-            // results, do not depend on it (only on when the pose flag is set).
-            const int qp = (ph == PH_STAGE) ? qpos : 0x7FFFFFFF;
-            const int m = min(__builtin_amdgcn_readlane(qp, 0), __builtin_amdgcn_readlane(qp, 32));
-#ifndef HC_ABORT_PRIO_DIV
-#define HC_ABORT_PRIO_DIV 16
-#endif
-            const int lvl = (int)((long long)m * HC_ABORT_PRIO_DIV / a.num_paths);
-            if (lvl <= 0) __builtin_amdgcn_s_setprio(3);
-            else if (lvl == 1) __builtin_amdgcn_s_setprio(2);
-            else if (lvl == 2) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        if (!ABORT && a.ordered && a.slice_q == 0) {
-            // Without time slicing: issue priority by queue position (s_setprio,
-            // arbitration among the waves of a SIMD): the last tenth of the
-            // queue at 3, the tenth before at 2, the one before that at 1.
-            // Paths dequeued late decide when the launch ends; the earlier
-            // ones have slack (profiles/r2_ab_priority.jsonl:
-            // -1.8 %).  With slicing it is neutral (profiles/r2n_ab_slice2.jsonl).
-            const int qp = (ph == PH_STAGE) ? qpos : 0;
-            const int m = max(__builtin_amdgcn_readlane(qp, 0), __builtin_amdgcn_readlane(qp, 32));
-            const int lvl = (int)((long long)m * PRIO_TENTHS / a.num_paths);
-            if (lvl >= PRIO_TENTHS - 1) __builtin_amdgcn_s_setprio(3);
-            else if (lvl >= PRIO_TENTHS - 2) __builtin_amdgcn_s_setprio(2);
-            else if (lvl >= PRIO_TENTHS - 3) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        if (!ABORT && a.slice_q > 0) {
-            // With time slicing: issue priority to the wave whose paths have
-            // run the fewest steps (least attained service): a path's remaining
-            // steps are bounded by max_steps - stepidx, so the paths that can
-            // still run longest get the larger share of their SIMD, and the
-            // launch ends with evenly short remainders.
-#ifndef HC_PRIO_REM
-#define HC_PRIO_REM 0
-#endif
-#if HC_PRIO_REM
-            // A/B: longest estimated remaining work first -- the steps left at
-            // dt doubling every 4 accepted steps, 4 log2(1 + (2^1/4 - 1)(1 - t0) / dt),
-            // capped by the steps the path may still take
-            const float est = 4.0f * __builtin_amdgcn_logf(1.0f + 0.1892f * (1.0f - t0) * __builtin_amdgcn_rcpf(dt));
-            int rem = a.max_steps - stepidx;
-            rem = (ph == PH_STAGE) ? min(rem, (int)est) : -1;
-            const int mr = max(__builtin_amdgcn_readlane(rem, 0), __builtin_amdgcn_readlane(rem, 32));
-            const int q4 = 3 - (int)((long long)max(mr, 0) * 4 / (a.max_steps + 1));
-#else
-            const int si = (ph == PH_STAGE) ? stepidx : (1 << 20);
-            const int m = min(__builtin_amdgcn_readlane(si, 0), __builtin_amdgcn_readlane(si, 32));
-            int q4 = (int)((long long)m * 4 / (a.max_steps + 1));
-#ifndef HC_PRIO_LAS
-#define HC_PRIO_LAS 1
-#endif
-            // A/B (HC_PRIO_LAS): 0 = one priority for all, -1 = most attained
-            // service first (a boost for the long paths)
-#ifdef HC_PRIO_STEPW
-            q4 = min(m / HC_PRIO_STEPW, 3);
-#endif
-            if (HC_PRIO_LAS == 0) q4 = 3;
-            if (HC_PRIO_LAS < 0) q4 = 3 - q4;
-#endif
-            if (q4 <= 0) __builtin_amdgcn_s_setprio(3);
-            else if (q4 == 1) __builtin_amdgcn_s_setprio(2);
-            else if (q4 == 2) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-        HC_DIAG_MARK(0);
-        // the found flag for the next step boundary: read now, used after the stage
-        if (ABORT && a.inflight_stop) {
-            found_seen = __hip_atomic_load(&ws->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // (the peer flag's xGMI round trip is hidden by the stage that follows)
-            if (a.peer_found) found_seen |= __hip_atomic_load(a.peer_found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-
-        // ---------------- one stage for both slots
-        // park the slot state in LDS so it does not occupy VGPRs across eval + LU
-        HC_ISA_MARK("ctl_park");
-        // the slot's prefix tables follow its p(t): rebuilt when t or the
-        // sample changed (about 0.4 times per stage and path; both halves of
-        // the wave rebuild when either needs it, each from its own t and sample)
-        const float pre_t = S.st.pre_t;
-        const int pre_smp = S.st.pre_smp;
-        const bool rebuild = __ballot(ph == PH_STAGE && (__float_as_uint(t0) != __float_as_uint(pre_t) ||
-                                                         smp_loaded != pre_smp)) != 0ull;
-        if (r == 0) {
-            SlotState q;
-            q.t0 = t0; q.t_step = t_step; q.dt = dt; q.h2 = h2; q.scale = scale;
-            q.s = s; q.stepidx = stepidx; q.coef = coef; q.succ = succ; q.nsteps = nsteps; q.ncorr = ncorr;
-            q.b = b; q.smp = smp_loaded; q.ph = ph;
-            q.flags = (end_zone ? 1 : 0) | (check ? 2 : 0) | (isSucc ? 4 : 0) | (isInf ? 8 : 0) | (piece << 4);
-            q.pad = qpos;
-            q.pre_t = rebuild ? t0 : pre_t;
-            q.pre_smp = rebuild ? smp_loaded : pre_smp;
-            S.st = q;
-        }
-        if (rl) { S.x[r] = x; S.xl[r] = xl; S.sols[r] = sols; }
-        if (rebuild) {
-            HC_ISA_MARK("ctl_prefix");
-#ifdef HC_DIAG_LUWORK
-            if (lane_fresh() == 0) atomicAdd(&g_diag_luwork[9], 1ull);
-#endif
-            const int rs = lane_fresh() & 31;   // == r; the LDS addresses are not hoisted and held across the loop
-            const size_t so = (size_t)(smp_loaded > 0 ? smp_loaded : 0) * NPP;
-            build_prefixes(S, rs, &T->pre[0][0], a.target_params + so, a.diff_params + so, s_sp, t0);
-        }
-        wave_lds_sync();
-        const int s_in = s, ph_in = ph;
-        asm volatile("" :: "v"(s_in), "v"(ph_in));
-        // opaque lane id: keeps LICM from hoisting ~30 lane-derived per-pivot
-        // constants (bpermute addresses, r == i masks) out of the path loop
-        const int lane_v = lane_fresh();   // recomputed (2 VALU), not held across the loop
-        const int r_v = lane_v & 31;
-        const uint32_t row_pat = s_rowc[GM_WORDS][r_v];
-        const bool act = ph_in == PH_STAGE;
-        const bool pred = act && s_in < 4;
-        HC_DIAG_MARK(1);
-        // the stage's linear system: right-hand side first (dH/dt | H need no
-        // Jacobian registers, so their LDS gathers can run many terms ahead),
-        // then dH/dx into rA
-        cf rB = cmk(0.0f, 0.0f);
-        HC_ISA_MARK("ev_rhs");
-        {
-            const bool any_p = __ballot(pred) != 0ull, any_c = __ballot(act && !pred) != 0ull;
-            const RhsMasks mk = rhs_masks(T);
-#ifdef HC_DIAG_LUWORK
-            if (lane_v == 0) atomicAdd(&g_diag_luwork[any_p && any_c ? 6 : any_p ? 7 : 8], 1ull);
-#endif
-            if (any_p && any_c) {                                            // :185 | :221, one pass
-                HC_ISA_MARK("ev_rhs_mixed");
-                rB = eval_rhs<RHS_MIXED>(s_ht, S, r_v, pred, mk);
-            } else if (any_p) {                                              // :185
-                HC_ISA_MARK("ev_rhs_ht");
-                const cf t = eval_rhs<RHS_HT>(s_ht, S, r_v, true, mk);
-                if (pred) rB = t;
-            } else if (any_c) {                                              // :221
-                HC_ISA_MARK("ev_rhs_h");
-                const cf t = eval_rhs<RHS_H>(s_ht, S, r_v, false, mk);
-                if (!pred) rB = t;
-            }
-        }
-        HC_DIAG_MARK(3);
-        cf rA[NV];
-        HC_ISA_MARK("ev_hx");
-        eval_hx(rA, s_hx, s_hxd, &s_rowc[0][0], S, r_v);                     // :184 / :220
-        wave_lds_sync();
-        HC_DIAG_MARK(2);
-        bool redo;
-        LUBuf &LB = *reinterpret_cast<LUBuf *>(S.lu);
-        // the LU's scratch: the dH/dx entry block, dead once gathered into rA
-        // (a dense re-solve evaluates dH/dx again)
-        static_assert(ENT_CAP >= LU_SCRATCH_CF && offsetof(SlotLDS, ent) % 16 == 0, "LU scratch in SlotLDS::ent");
-#ifdef HC_DIAG_LUWORK
-        cf k = lu_solve<false, LUCH, LULAT, LUSTRUCT>(rA, rB, lane_v, row_pat, LB, S.ent, redo, __ballot(act));   // :188 / :224
-#else
-        cf k = lu_solve<false, LUCH, LULAT, LUSTRUCT>(rA, rB, lane_v, row_pat, LB, S.ent, redo);                  // :188 / :224
-#endif
-        HC_ISA_MARK("ctl_redo");
-        if (__builtin_expect(redo, 0)) {
-            // a system the sparse solve cannot take exactly (an entry not provably
-            // finite, a pivot outside the fast reciprocal range): dH/dx and the
-            // right-hand side are evaluated again (the sparse solve used the
-            // entry block as its scratch), and the system solved densely
-            // (the stage kind re-read from the parked slot state: held across the
-            // LU, act / pred would be spilled)
-            HC_ISA_MARK("redo_evals");
-            const bool act_r = S.st.ph == PH_STAGE, pred_r = act_r && S.st.s < 4;
-            // a fresh lane id: the table addresses of the stage's evaluations
-            // are not shared with (and held across the LU for) this rare path
-            const int r_r = lane_fresh() & 31;
-            cf rb = cmk(0.0f, 0.0f);
-            if (__ballot(pred_r) != 0ull) {
-                const cf t = eval_rhs<RHS_HT>(s_ht, S, r_r, true, rhs_masks(T));
-                if (pred_r) rb = t;
-            }
-            if (__ballot(act_r && !pred_r) != 0ull) {
-                const cf t = eval_rhs<RHS_H>(s_ht, S, r_r, false, rhs_masks(T));
-                if (!pred_r) rb = t;
-            }
-            // (eval_hx without its phase marker: the ISA phase count keeps this rare
-            // copy under redo_evals)
-            eval_hx_terms(s_hx, s_hxd, reinterpret_cast<char *>(&S), r_r);
-            wave_lds_sync();
-            gather_hx(rA, &s_rowc[0][0], S, r_r);
-            wave_lds_sync();
-#ifdef HC_DIAG_LUWORK
-            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, S.ent, redo, __ballot(act_r));
-#else
-            k = lu_solve<true, LUCH>(rA, rb, lane_v, row_pat, LB, S.ent, redo);
-#endif
-        }
-        wave_lds_sync();
-#ifdef HC_DIAG_PHASES
-        {   // [4] forward elimination up to the solve's boundary stamp, [5] the rest of the LU
-            const uint64_t mid = g_diag_lu_mid[blockIdx.x * 4 + wid];
-            const uint64_t n_ = __builtin_amdgcn_s_memtime();
-            if (mid > dt_ && mid < n_) { dg[4] += mid - dt_; dt_ = mid; }
-        }
-#endif
-        HC_DIAG_MARK(5);
-        HC_ISA_MARK("ctl_update");
-        {
-            const SlotState q = S.st;
-            t0 = q.t0; t_step = q.t_step; dt = q.dt; h2 = q.h2; scale = q.scale;
-            s = q.s; stepidx = q.stepidx; coef = q.coef; succ = q.succ; nsteps = q.nsteps; ncorr = q.ncorr;
-            b = q.b; smp_loaded = q.smp; ph = q.ph;
-            end_zone = q.flags & 1; check = q.flags & 2; isSucc = q.flags & 4; isInf = q.flags & 8;
-            piece = q.flags >> 4;
-            qpos = q.pad;
-            x = rl ? S.x[r] : cmk(0.0f, 0.0f);
-            xl = rl ? S.xl[r] : cmk(0.0f, 0.0f);
-            sols = rl ? S.sols[r] : cmk(0.0f, 0.0f);
-        }
-        // act / pred of this stage, from the reloaded state
-        const bool act_q = ph == PH_STAGE, pred_q = act_q && s < 4;
-        if (act_q) {
-            bool step_end = false;
-            if (pred_q) {
-                if (ARCH && s < 3 && a.explicit_rk) {
-                    // archived ..._PH.cu with dev-get-new-data.cuh:37-71, gc = MAGMA_C_ONE:
-                    // s += ((k*dt)*gc*1.0)/(6|3); x = (s ? x_last : x) + k*((h2|dt)*gc)
-                    const cf kd = cmul(cscale(k, dt), cmk(1.0f, 0.0f));
-                    sols = cadd(sols, cdivs(cscale(kd, 1.0f), s == 0 ? 6.0f : 3.0f));
-                    if (s > 0) x = xl;
-                    x = cadd(x, cmul(k, cmk(s == 2 ? dt : h2, 0.0f)));
-                    if (s != 1) t0 += h2;
-                } else if (s < 3) {                                          // :191-205
-                    // (double)coef * 1.0 / 6.0 rounded to float; coef is 1 or 2 here
-                    // (it doubles after s = 0 and s = 2): a constant each, so no f64 division
-                    const float w = coef == 1   ? (float)(1.0 / 6.0)
-                                    : coef == 2 ? (float)(2.0 / 6.0)
-                                                : (float)((double)coef * 1.0 / 6.0);
-                    sols = cadd(sols, cscale(cscale(k, dt), w));
-                    if (coef > 1) x = xl;
-                    const int sc = (s == 1) ? 0 : 1;
-                    scale += (float)sc * h2;
-                    coef <<= sc;
-                    x = cadd(x, cscale(k, scale));
-                    t0 += (float)sc * h2;
-                } else {                                                     // :209-210
-                    sols = cadd(sols, cdivs(cscale(cscale(k, dt), 1.0f), 6.0f));
-                    x = sols;
-                }
-                s++;
-                if (s == 4 && a.max_corr <= 0) step_end = true;
-            } else {                                                         // :228-249
-                x = csub(x, k);
-                ncorr++;
-                const float vs = rl ? k.x * k.x + k.y * k.y : 0.0f;
-                const float vc = rl ? x.x * x.x + x.y * x.y : 0.0f;
-                const float ns = tree_sum_half(vs), nc = tree_sum_half(vc);
-                isSucc = (double)ns < 0.000001 * (double)nc;
-                isInf = (double)nc > 1e14;
-                if (isInf || isSucc || (s - 4) + 1 >= a.max_corr) step_end = true;
-                else s++;
-            }
-            if (step_end) {
-                if (isInf) {                                                 // :252
-                    ph = PH_FINISH;
-                } else {
-                    if (!isSucc) {                                           // :257-265
-                        dt = (float)((double)dt * 0.5);
-                        x = xl;
-                        sols = xl;
-                        succ = 0;
-                        t0 = t_step;
-                    } else {                                                 // :266-275
-                        succ++;
-                        xl = x;
-                        sols = x;
-                        if (succ >= a.inc_steps) { succ = 0; dt *= 2.0f; }
-                    }
-                    stepidx++;
-                    ph = PH_BEGIN;
-                }
-            }
-        }
-    }
-#ifdef HC_DIAG_TIMES
-    if (lane == 0) {
-        const unsigned long long w1 = __builtin_amdgcn_s_memrealtime();
-        atomicMax(&g_diag_span[1], w1);
-        atomicAdd(&g_diag_span[2], w1 - diag_w0);
-        atomicAdd(&g_diag_span[3], 1ull);
-    }
-#endif
-#ifdef HC_DIAG_PHASES
-    HC_DIAG_MARK(0);
-    if (lane == 0) {
-        dg[7] = __builtin_amdgcn_s_memtime() - dt0_;
-        for (int q = 0; q < 8; q++) atomicAdd(&g_diag_phase[q], (unsigned long long)dg[q]);
-        atomicAdd(&g_diag_phase[8], 1ull);
-    }
-#endif
-#undef HC_DIAG_MARK
+// Tracking launches that fill at most half of the path slots: the SIMDs are
+// short of waves, a path's latency sets the launch time, and the latency-mode
+// LU is faster (profiles/r6y_ab_small_launch.jsonl: 1-8 samples -16..-19 %,
+// 16 samples -5 %, 24 equal, 100 +9 %).  The same body as k_track.
+template <bool LUS>
+__global__ void __launch_bounds__(WG_THREADS, 5) k_track_small(KArgs a) {
+    constexpr bool ABORT = false, GTAB = true, ARCH = false;
+    constexpr int LUCH = LU_CHUNK;
+    constexpr int LULAT = HC_LU_LATB_COLS;
+#include "hc_track_body.inc"
 }
 
 // ---------------------------------------------------------------- components
@@ -1591,6 +1013,9 @@ static size_t ws_bytes_for(long long paths, int max_steps) {
 // tests only (hc_trifocal_set_ring_test, include/hc_trifocal_testing.h): pusher
 // delay of every 16th ring ticket; read by every launch of every thread
 static std::atomic<int> g_ring_test{0};
+// tests only (hc_trifocal_set_small_launch): -1 never the small-launch
+// kernels, 0 by size, 1 always (tracking launches)
+static std::atomic<int> g_small_launch{0};
 
 // Persistent grid: resident workgroups (occupancy API, cached per device and
 // kernel) x CUs, capped by the work.
@@ -1699,6 +1124,19 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     const void *kern_any = abort_mode ? (const void *)k_track<true, HC_ABORT_MINW, HC_ABORT_GTAB, false, false>
                            : archived ? (const void *)k_track<false, 5, true, true, false>
                                       : (const void *)k_track<false, 5, true, false, false>;
+#ifndef HC_SMALL_LAUNCH
+#define HC_SMALL_LAUNCH 1
+#endif
+    const int small_mode = g_small_launch.load(std::memory_order_relaxed);
+    if (HC_SMALL_LAUNCH && !abort_mode && !archived && small_mode >= 0) {
+        // at most half of the path slots filled (or forced by the testing
+        // hook): the latency-mode instantiations
+        const long long slots = 2ll * WAVES_PER_WG * grid_for(0x40000000, kern);
+        if (small_mode > 0 || (slots > 0 && 2 * paths <= slots)) {
+            kern = (const void *)k_track_small<true>;
+            kern_any = (const void *)k_track_small<false>;
+        }
+    }
     const int grid = grid_for((int)((paths + 1) / 2), kern);
     const int grid_any = grid_for((int)((paths + 1) / 2), kern_any);
     if (grid <= 0 || grid_any <= 0) return HC_ERROR_DEVICE;
@@ -2000,12 +1438,17 @@ void hc_trifocal_set_ring_test(int delay_ticks) {
                           std::memory_order_relaxed);
 }
 
+void hc_trifocal_set_small_launch(int mode) {
+    hc::g_small_launch.store(mode < 0 ? -1 : mode > 0 ? 1 : 0, std::memory_order_relaxed);
+}
+
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.5 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+    return "hc_trifocal gfx950 v10.6 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
            "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
            "column groups by structural class (never-fillable groups untested, always-live groups unconditional), "
            "pivot search narrowed to the candidate rows' DPP group "
-           "(abort kernel: batched latency mode, one LDS round trip per pivot step, every live-able column group untested), "
+           "(abort kernel and tracking launches filling at most half of the path slots: batched latency mode, one LDS "
+           "round trip per pivot step, every live-able column group untested), "
            "structure-agnostic twin kernels for other dH/dx structures, readlane back substitution, pipelined evals over "
            "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
            "issue priority)";
