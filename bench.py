@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--samples", type=int, default=100, help="RANSAC samples per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-small-launch", action="store_true",
+                    help="skip the 1- and 8-sample launch timings (profiles: keeps the kernel trace to config 2)")
     ap.add_argument("--cpu-samples", type=int, default=160,
                     help="samples in the bounded CPU baseline run (~15 s on 16 host cores)")
     ap.add_argument("--abort-samples", type=int, default=1000,
@@ -315,6 +317,28 @@ def main():
     launch_ms = np.array([a_.elapsed_time(b_) for a_, b_ in ev])
     # every rank's own kernel time (median of its 5 single launches) and wall time per step
     rank_ms = gather_floats([float(np.median(launch_ms)), el_own * 1e3 / args.steps], dev, world)
+
+    # small launches (1 and 8 samples): the latency-mode tracking kernel the
+    # launcher picks when a launch fills at most half of the path slots, against
+    # the throughput kernel forced (hc_trifocal_set_small_launch)
+    small = {"samples": [] if args.no_small_launch else [1, 8], "latency_kernel_ms": [], "throughput_kernel_ms": []}
+    for n in small["samples"]:
+        sb = tr.allocate(n)
+        for mode, key in ((0, "latency_kernel_ms"), (-1, "throughput_kernel_ms")):
+            _abi.lib().hc_trifocal_set_small_launch(mode)
+            try:
+                sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(6)]
+                for a_, b_ in sev:
+                    tr.reset_tracks(sb)
+                    a_.record(stream)
+                    tr.launch(tgt[:n], dif[:n], sb, stream=stream)
+                    b_.record(stream)
+                torch.cuda.synchronize(dev)
+            finally:
+                _abi.lib().hc_trifocal_set_small_launch(0)
+            small[key].append(round(float(np.median([a_.elapsed_time(b_) for a_, b_ in sev[1:]])), 4))
+        del sb
+    tr.workspace_status()
 
     # the papers' ablation ladder: the same launch through the archived
     # ..._PH (explicit RK, no truncation) and ..._PH_CodeOpt (no truncation) semantics
@@ -547,6 +571,10 @@ def main():
                                f"reset tracks + one tracking launch, steps rotating over {NS} streams",
                        "single_launch_paths_per_s": round(paths / (float(np.median(launch_ms)) / 1e3), 1),
                        "pipelined_paths_per_s": None if pipelined is None else round(pipelined, 1),
+                       "small_launch": dict(small, note="ms per tracking launch of 1 / 8 samples (median of 5, HIP "
+                                                         "events): the latency-mode kernel the launcher picks at "
+                                                         "most half of the path slots, and the throughput kernel "
+                                                         "forced"),
                        "pipelined_streams": args.pipelined_streams if pipelined is not None else None,
                        "pipelined_note": "the same K steps with consecutive batches overlapped on "
                                          f"{args.pipelined_streams} streams (own buffers each): a batch's "

@@ -43,7 +43,7 @@ for step in ${STEPS//,/ }; do
     luwork) HC_TRIFOCAL_LIB=$L/libhc_trifocal_luwork.so run luwork 200 python scripts/lu_work.py > $O/${T}_lu_work.json; rc=$?; cat $O/${T}_lu_work.json ;;
     bench) run bench 600 python bench.py $BENCH_ARGS > $O/${T}_bench.json 2> $O/${T}_bench.err; rc=$?; cat $O/${T}_bench.json ;;
     profile|traffic)
-      B="python bench.py --steps 30 --warmup 3 --no-cpu-baseline --abort-samples 0 --noisy-trials 0 --streams 1 --pipelined-streams 0"
+      B="python bench.py --steps 30 --warmup 3 --no-cpu-baseline --no-small-launch --abort-samples 0 --noisy-trials 0 --streams 1 --pipelined-streams 0"
       run trace 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${T}_trace -o run -- $B > $O/${T}_trace.log 2>&1; rc=$?
       if [ $step = profile ]; then
         SETS=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_WAIT_ANY"
