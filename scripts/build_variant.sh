@@ -4,6 +4,8 @@
 # -DHC_DIAG_TIMES [-DHC_DIAG_UTIL], -DHC_DIAG_LUWORK).  The round-2 A/B switches
 # (HC_LU_*, HC_EV_*, HC_HX_GROUPED, HC_AB_*, HC_CGESV4, HC_SLICE_Q, HC_PRIO_*)
 # were removed from the product sources in round 3; they live in commit 136b029.
+# Round 6's scheduling switches (HC_SLICE_HOLD, HC_PRIO_LAS, HC_PRIO_STEPW,
+# HC_PRIO_REM) live in commit 02bc69d.
 set -e
 cd "$(dirname "$0")/../trifocal_pose_estimation_using_improved_gpuhc_amd/csrc"
 N=$1; shift
