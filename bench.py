@@ -171,10 +171,16 @@ def spawn_ranks(gpus, argv):
     import subprocess
     env = dict(os.environ, HC_BENCH_SPAWNED="1")
     try:
-        return subprocess.run(spawn_command(gpus, argv, free_port()), env=env).returncode or 0
+        # the ranks' stdout through a pipe: rank 0's JSON line to stdout, anything
+        # else the ranks or their backend libraries print to stderr, so that
+        # stdout holds the one bench line
+        p = subprocess.Popen(spawn_command(gpus, argv, free_port()), env=env, stdout=subprocess.PIPE, text=True)
     except OSError as e:
         print(f"[bench] could not start {gpus} ranks: {e}", file=sys.stderr)
         return 1
+    for line in p.stdout:
+        print(line, end="", file=sys.stdout if line.startswith('{"metric"') else sys.stderr, flush=True)
+    return p.wait() or 0
 
 
 def rank_abort_record(g, runs, shard_paths, chunk_paths):

@@ -41,6 +41,19 @@ def test_spawn_command_runs_this_script_per_gpu():
     assert os.path.samefile(cmd[-5], os.path.join(ROOT, "bench.py"))
 
 
+def test_spawned_ranks_stdout_carries_only_the_bench_line(monkeypatch, capsys):
+    # what a backend library prints on the ranks' stdout (gloo's connection
+    # lines) goes to stderr; the bench line and the ranks' exit code pass through
+    script = "print('[Gloo] Rank 1 is connected to 1 peer ranks.'); print('{\"metric\": \"m\", \"value\": 1}'); " \
+             "print('trailing'); raise SystemExit(3)"
+    monkeypatch.setattr(bench, "spawn_command", lambda gpus, argv, port: [sys.executable, "-c", script])
+    rc = bench.spawn_ranks(2, [])
+    out, err = capsys.readouterr()
+    assert rc == 3
+    assert out.splitlines() == ['{"metric": "m", "value": 1}']
+    assert "[Gloo]" in err and "trailing" in err
+
+
 def test_bench_line_fields_from_helpers():
     # the algorithmic bytes of config 2: ~0.5 KB per path
     b = bench.algorithmic_bytes(100)
