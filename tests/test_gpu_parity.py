@@ -282,6 +282,46 @@ def test_time_slicing_concurrent_streams(problem, samples100, tracker):
         assert np.array_equal(h["tracks"].view(np.uint32), ref["tracks"].view(np.uint32))
 
 
+def test_small_and_large_launches_share_a_workspace(problem, samples100, tracker):
+    """One workspace, launches of 100, 8, 100 and 2 samples: the launcher
+    alternates between the throughput kernel (k_track) and the latency-mode
+    one (k_track_small), which keep the same control block, tables and ring;
+    then four 8-sample launches in flight at once on four streams (own
+    buffers and workspaces).  Every launch equals the serial run bit for bit."""
+    import torch
+    tgt, dif, _ = samples100
+    ref = tracker.track(tgt, dif, time_slicing=False).host()
+    dev = tracker.device
+    t, d = torch.from_numpy(tgt).to(dev), torch.from_numpy(dif).to(dev)
+
+    def check(h, n):
+        sl = slice(0, n * 312)
+        assert (h["converge"] == ref["converge"][sl]).all() and (h["infinity"] == ref["infinity"][sl]).all()
+        assert np.array_equal(h["stats"]["steps"], ref["stats"]["steps"][sl])
+        assert np.array_equal(h["tracks"].view(np.uint32), ref["tracks"][sl].view(np.uint32))
+
+    ws = tracker.new_workspace(100)
+    for n in (100, 8, 100, 2):
+        r = tracker.allocate(n)
+        tracker.reset_tracks(r)
+        tracker.launch(t, d, r, workspace=ws, num_samples=n)
+        torch.cuda.synchronize(dev)
+        assert int(tracker.L.hc_trifocal_workspace_status(ctypes.c_void_p(ws.data_ptr()))) == 0
+        check(r.host(), n)
+    streams = [torch.cuda.Stream(dev) for _ in range(4)]
+    bufs = [tracker.allocate(8) for _ in range(4)]
+    wss = [tracker.new_workspace(8) for _ in range(4)]
+    torch.cuda.synchronize(dev)
+    for k in range(4):
+        with torch.cuda.stream(streams[k]):
+            tracker.reset_tracks(bufs[k])
+        tracker.launch(t, d, bufs[k], stream=streams[k], workspace=wss[k], num_samples=8)
+    torch.cuda.synchronize(dev)
+    for k in range(4):
+        assert int(tracker.L.hc_trifocal_workspace_status(ctypes.c_void_p(wss[k].data_ptr()))) == 0
+        check(bufs[k].host(), 8)
+
+
 def test_time_slicing_falls_back_when_the_ring_does_not_fit(problem, samples100, tracker):
     """A workspace sized for a smaller GPUHC_Max_Steps than the launch uses
     (hc_trifocal_workspace_size_for_steps) cannot hold one ring entry per
