@@ -10,7 +10,9 @@
             paths equal the oracle's tracks of the same batch ids, skipped
             paths are untouched;
   gate 2     reference-independent: every converged real
-            solution of config 2 satisfies the target system in FP64.
+            solution of config 2 satisfies the target system in FP64;
+  largest   config 4's whole workload (8000 samples) in one tracking launch
+            on one GPU: the golden prefix, oracle paths across the launch.
 """
 import os
 
@@ -92,6 +94,44 @@ def test_residual_gate_config2(problem, samples100, tracker):
     assert len(ids) > 0
     worst = max_relative_residual(problem.dHdt_index, r["tracks"], ids, tgt)
     assert worst <= RESIDUAL_TOL, worst
+
+
+def test_largest_launch_config4_workload_on_one_gpu(problem, oracle, tracker, ransac0):
+    """The largest launch: config 4's whole workload, 8000 samples (2 496 000
+    paths), in one tracking launch on one GPU with time slicing (its ring and
+    suspend blocks: 1.2 GB).  Samples are independent and their srand(0) draws
+    are one sequence, so the first 100 samples equal the N = 100 golden run;
+    700 paths drawn across the launch equal the oracle's tracks of the same
+    batch ids; every suspended path was resumed."""
+    import sys
+
+    import torch
+
+    from trifocal_pose_estimation_using_improved_gpuhc_amd import prepare_target_params
+    sys.path.insert(0, GOLDEN)
+    from make_golden import track_hash
+    N = 8000
+    tgt, dif, _ = prepare_target_params(problem, ransac0, seed=0, num_samples=N)
+    r = tracker.track(tgt, dif)
+    off = int(tracker.L.hc_trifocal_workspace_size())
+    rq = np.frombuffer(tracker.workspace[off:off + 768].cpu().numpy().tobytes(), np.uint32)
+    assert rq[64] > 100000 and rq[0] == rq[64] and rq[128] == 0, "sliced, and every suspended path resumed"
+    st = r.stats.cpu().numpy().view(np.int32).reshape(-1, 4)
+    assert (st[:, 0] >= 1).all() and (st[:, 0] <= tracker.settings.max_steps + 1).all()
+    g = np.load(os.path.join(GOLDEN, "gpuhc_N100_seed0.npz"))
+    n0 = 100 * 312
+    assert np.array_equal(r.converge[:n0].cpu().numpy(), g["conv"])
+    assert np.array_equal(r.infinity[:n0].cpu().numpy(), g["inf"])
+    assert np.array_equal(st[:n0, 0], g["steps"]) and np.array_equal(st[:n0, 1], g["corrections"])
+    assert (track_hash(r.tracks[:n0].cpu().numpy()) == g["hash"]).all()
+    ids = np.sort(np.random.default_rng(7).choice(N * 312, 700, replace=False))
+    idx = torch.from_numpy(ids).to(r.tracks.device)
+    o_tr, o_conv, o_inf, o_st = oracle.gpuhc_track_subset(ids, problem.start_sols, problem.start_params, tgt, dif,
+                                                          problem.unified_index)
+    assert np.array_equal(r.converge[idx].cpu().numpy(), o_conv[ids])
+    assert np.array_equal(r.infinity[idx].cpu().numpy(), o_inf[ids])
+    assert np.array_equal(st[ids, 0], o_st["steps"][ids]) and np.array_equal(st[ids, 1], o_st["corrections"][ids])
+    assert same(r.tracks[idx].cpu().numpy()[:, :30], o_tr[ids, :30]).all()
 
 
 @pytest.mark.parametrize("inflight_stop", [0, 1])
