@@ -1018,7 +1018,7 @@ static std::atomic<int> g_ring_test{0};
 static std::atomic<int> g_small_launch{0};
 
 // Persistent grid: resident workgroups (occupancy API, cached per device and
-// kernel) x CUs, capped by the work.
+// kernel) x CUs, capped by the work.  resident_wgs(k) = grid_for(INT_MAX, k).
 static int grid_for(int waves_needed, const void *kernel) {
     static std::mutex mu;
     static std::map<std::pair<int, const void *>, std::pair<int, int>> cache;   // -> (CUs, workgroups per CU)
@@ -1037,10 +1037,11 @@ static int grid_for(int waves_needed, const void *kernel) {
         cus = it->second.first;
         per_cu = it->second.second;
     }
-    const int want = (waves_needed + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    const int want = waves_needed / WAVES_PER_WG + (waves_needed % WAVES_PER_WG != 0);
     const int cap = cus * per_cu;
     return want < cap ? want : cap;
 }
+static int resident_wgs(const void *kernel) { return grid_for(INT_MAX, kernel); }
 
 static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *workspace, size_t wsb,
                              hcStream stream, bool abort_mode, bool truncate = true, bool explicit_rk = false) {
@@ -1131,7 +1132,7 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     if (HC_SMALL_LAUNCH && !abort_mode && !archived && small_mode >= 0) {
         // at most half of the path slots filled (or forced by the testing
         // hook): the latency-mode instantiations
-        const long long slots = 2ll * WAVES_PER_WG * grid_for(0x40000000, kern);
+        const long long slots = 2ll * WAVES_PER_WG * resident_wgs(kern);   // two paths per wave
         if (small_mode > 0 || (slots > 0 && 2 * paths <= slots)) {
             kern = (const void *)k_track_small<true>;
             kern_any = (const void *)k_track_small<false>;
