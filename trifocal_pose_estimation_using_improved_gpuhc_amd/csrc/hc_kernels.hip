@@ -886,12 +886,21 @@ __global__ void __launch_bounds__(WG_THREADS, MINW) k_track(KArgs a) {
 // Tracking launches that fill at most half of the path slots: the SIMDs are
 // short of waves, a path's latency sets the launch time, and the latency-mode
 // LU is faster (profiles/r6y_ab_small_launch.jsonl: 1-8 samples -16..-19 %,
-// 16 samples -5 %, 24 equal, 100 +9 %).  The same body as k_track.
+// 16 samples -5 %, 24 equal, 100 +9 %).  The same body as k_track.  Such a
+// launch needs few waves, so the registers go to 3 waves/SIMD: no spills and
+// 16 columns per LU batch (profiles/r7g_ab_small_occupancy.jsonl: a further
+// -5 % at 1-4 samples, -4..-7 % at 8-16; 6144 path slots)
+#ifndef HC_SMALL_MINW
+#define HC_SMALL_MINW 3
+#endif
+#ifndef HC_SMALL_LAT
+#define HC_SMALL_LAT 16
+#endif
 template <bool LUS>
-__global__ void __launch_bounds__(WG_THREADS, 5) k_track_small(KArgs a) {
+__global__ void __launch_bounds__(WG_THREADS, HC_SMALL_MINW) k_track_small(KArgs a) {
     constexpr bool ABORT = false, GTAB = true, ARCH = false;
     constexpr int LUCH = LU_CHUNK;
-    constexpr int LULAT = HC_LU_LATB_COLS;
+    constexpr int LULAT = HC_SMALL_LAT;
 #include "hc_track_body.inc"
 }
 
@@ -1130,10 +1139,12 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
 #endif
     const int small_mode = g_small_launch.load(std::memory_order_relaxed);
     if (HC_SMALL_LAUNCH && !abort_mode && !archived && small_mode >= 0) {
-        // at most half of the path slots filled (or forced by the testing
+        // at most half of the throughput kernel's path slots filled, and every
+        // path in a slot of the small kernel at once (or forced by the testing
         // hook): the latency-mode instantiations
         const long long slots = 2ll * WAVES_PER_WG * resident_wgs(kern);   // two paths per wave
-        if (small_mode > 0 || (slots > 0 && 2 * paths <= slots)) {
+        const long long small_slots = 2ll * WAVES_PER_WG * resident_wgs((const void *)k_track_small<true>);
+        if (small_mode > 0 || (slots > 0 && 2 * paths <= slots && paths <= small_slots)) {
             kern = (const void *)k_track_small<true>;
             kern_any = (const void *)k_track_small<false>;
         }
@@ -1444,12 +1455,13 @@ void hc_trifocal_set_small_launch(int mode) {
 }
 
 const char *hc_trifocal_version(void) {
-    return "hc_trifocal gfx950 v10.6 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
+    return "hc_trifocal gfx950 v10.7 (2 paths/wave, structurally sparse LDS-broadcast LU with lean pivot steps, "
            "one exec region per pivot step for the eligible rows with the column groups through scratch windows, "
            "column groups by structural class (never-fillable groups untested, always-live groups unconditional), "
            "pivot search narrowed to the candidate rows' DPP group "
-           "(abort kernel and tracking launches filling at most half of the path slots: batched latency mode, one LDS "
-           "round trip per pivot step, every live-able column group untested), "
+           "(abort kernel and tracking launches filling at most half of the path slots -- the latter at 3 waves/SIMD, "
+           "16 columns per batch: batched latency mode, one LDS round trip per pivot step, every live-able column "
+           "group untested), "
            "structure-agnostic twin kernels for other dH/dx structures, readlane back substitution, pipelined evals over "
            "per-slot prefix tables, 5 waves/SIMD, time slicing at step boundaries with least-attained-service "
            "issue priority)";
