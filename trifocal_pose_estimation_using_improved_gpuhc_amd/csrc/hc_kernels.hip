@@ -58,13 +58,12 @@ struct Workspace {
     unsigned queue;          // path work queue
     unsigned status;         // HC_ERROR_TABLE if the index table does not fit the compaction
     unsigned found;          // device-side "good hypothesis found" flag
-    unsigned finished;       // paths finished (tail hand-over, HC_HANDOVER)
+    unsigned pad0;
     unsigned long long t_start;   // s_memrealtime when the first workgroup started (abort mode)
     unsigned long long t_found;   // s_memrealtime of the first good hypothesis
     unsigned ring_fail[4];   // time slicing: ticket, tag seen, tail, head of a ring entry that never came (diagnostics)
     unsigned abandoned;      // time slicing: ring tickets abandoned by their consumers (re-pushed; diagnostics)
-    unsigned handover;       // tail hand-over flag (HC_HANDOVER)
-    unsigned pad1[2];
+    unsigned pad1[3];
     // written by k_prep_tables
     EvalTables tab;
 };
@@ -137,12 +136,6 @@ __device__ __forceinline__ unsigned long long ring_wait_ticks(int ring_test) {
     return ring_test > 0 ? (unsigned long long)(ring_test / 8) : RING_ABANDON_TICKS;
 }
 
-#ifndef HC_HANDOVER
-#define HC_HANDOVER 0
-#endif
-#ifndef HC_HANDOVER_DIV
-#define HC_HANDOVER_DIV 2
-#endif
 struct KArgs {
     int num_paths;
     int ordered;        // dequeue track-major in c_track_order (abort mode off)
@@ -175,9 +168,6 @@ struct KArgs {
     unsigned *rq;                   // ring counters, one 256-B line each: [0] head, [64] tail, [128] avail, [192] meta
     unsigned long long *susp;       // suspend blocks, SUSP_WORDS per path id
     unsigned long long *ring;       // ring_tag(epoch, ticket) << 32 | path id
-#if HC_HANDOVER
-    int handover_at;                // tail hand-over: remaining paths at which the halves leave for k_track_small (0 off)
-#endif
 };
 // rq layout: counters zeroed by k_prep_tables every launch; meta: the launch
 // epoch, a magic word and the ring entries already cleared (persist)
@@ -1171,25 +1161,6 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
         k.found_flag = ab->found_trifocal_sols;
         k.batch_index = ab->trifocal_sols_batch_index;
     }
-#if HC_HANDOVER
-    // tail hand-over (sliced tracking launches larger than the small kernel's
-    // share): once few paths remain, k_track's halves push their paths to the
-    // ring at their next slice boundary and exit; k_track_small, enqueued
-    // behind it, resumes them with the latency-mode LU
-    KArgs kb = k;
-    int grid_b = 0;
-    if (k.rq && !abort_mode && !archived && kern == (const void *)k_track<false, 5, true>) {
-        const long long small_slots = 2ll * WAVES_PER_WG * resident_wgs((const void *)k_track_small<true>);
-        const long long slots = 2ll * WAVES_PER_WG * resident_wgs(kern);
-        const long long t = small_slots < slots / HC_HANDOVER_DIV ? small_slots : slots / HC_HANDOVER_DIV;
-        if (t > 0 && paths > t) {
-            k.handover_at = (int)t;
-            kb.handover_at = 0;
-            grid_b = grid_for((int)((t + 1) / 2), (const void *)k_track_small<true>);
-            if (grid_b <= 0) return HC_ERROR_DEVICE;
-        }
-    }
-#endif
     void *kargs[] = {&k};
     g_last_hip_error = hipLaunchKernel(kern, dim3(grid), dim3(WG_THREADS), kargs, 0, s);
     if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
@@ -1197,16 +1168,6 @@ static hcStatus launch_track(const hcTrackArgs *t, const hcAbortArgs *ab, void *
     g_last_hip_error = hipLaunchKernel(kern_any, dim3(grid_any), dim3(WG_THREADS), kargs, 0, s);
     if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
     if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-#if HC_HANDOVER
-    if (grid_b > 0) {
-        void *kargsb[] = {&kb};
-        for (const void *kk : {(const void *)k_track_small<true>, (const void *)k_track_small<false>}) {
-            g_last_hip_error = hipLaunchKernel(kk, dim3(grid_b), dim3(WG_THREADS), kargsb, 0, s);
-            if (g_last_hip_error != hipSuccess) return HC_ERROR_LAUNCH;
-            if (launch_status(HC_ERROR_LAUNCH) != HC_SUCCESS) return HC_ERROR_LAUNCH;
-        }
-    }
-#endif
     if (k.rq) {   // a suspended path that was never resumed is reported, not left stale
         hipLaunchKernelGGL(k_ring_check, dim3(1), dim3(64), 0, s, ws, (const unsigned *)k.rq);
         return launch_status(HC_ERROR_LAUNCH);
