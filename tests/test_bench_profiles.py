@@ -54,3 +54,28 @@ def test_wilson_interval():
     assert abs(lo - 0.3127) < 1e-3 and abs(hi - 0.8318) < 1e-3
     assert bench.wilson95(0, 30)[0] == 0.0 and bench.wilson95(30, 30)[1] == 1.0
     assert bench.wilson95(0, 0) is None
+
+
+def test_committed_bench_line_keeps_the_contract():
+    """The shipped build's committed bench line (profiles/r7i_bench.json) carries
+    every field of the driver's contract, a roofline and CPU baseline of the
+    right shape, the HBM traffic of its own build, and small launches faster
+    on the latency-mode kernel than on the throughput one."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = json.load(open(os.path.join(root, "profiles", "r7i_bench.json")))
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "f32"
+    assert abs(d["value"] - 31200 / (d["ms_per_step"] / 1e3)) / d["value"] < 1e-3
+    assert "config 2" in d["config"]["workload"]
+    r = d["roofline"]
+    assert {"bound", "achieved", "peak", "unit", "frac", "traffic"} <= set(r)
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3 and 0 < r["frac"] < 1
+    assert r["traffic_source"] == "profiles/r7i_pmc_summary.json"
+    c = d["cpu_baseline"]
+    assert {"value", "unit", "cores", "kind", "sample"} <= set(c) and c["kind"] in ("port", "reference")
+    s = d["config"]["small_launch"]
+    assert s["samples"] == [1, 8]
+    assert all(a < b for a, b in zip(s["latency_kernel_ms"], s["throughput_kernel_ms"]))
+    assert d["config"]["build_id"] == json.load(open(os.path.join(root, r["traffic_source"])))["build_id"]
